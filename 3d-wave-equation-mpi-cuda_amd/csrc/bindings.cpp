@@ -1,0 +1,301 @@
+// Python binding of libwave3d (pybind11; deliberately no libtorch dependency — tensors
+// cross the boundary as raw device pointers + the caller's HIP stream).
+//
+//   run(args, backend, transport)  whole solver runs (CLI-equivalent), returns a dict
+//   RcclTransport / rccl_unique_id native RCCL halo transport (bootstrapped from Python)
+//   Transport                      subclassable from Python (e.g. torch.distributed/gloo)
+//   k_* functions                  the individual HIP kernels, for numerics tests
+#include <hip/hip_runtime.h>
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include "checkpoint.hpp"
+#include "hip_kernels.hpp"
+#include "problem.hpp"
+#include "rccl_transport.hpp"
+#include "solver.hpp"
+
+namespace py = pybind11;
+using namespace wave3d;
+
+namespace {
+
+// Host transport implemented in Python. `exchange(sends, recvs)` receives lists of
+// (peer, tag, address, nbytes); the Python side must complete all transfers.
+class PyTransport : public Transport {
+public:
+    using Transport::Transport;
+    std::string name() const override { PYBIND11_OVERRIDE_PURE(std::string, Transport, name); }
+    int rank() const override { PYBIND11_OVERRIDE_PURE(int, Transport, rank); }
+    int size() const override { PYBIND11_OVERRIDE_PURE(int, Transport, size); }
+    bool device() const override { PYBIND11_OVERRIDE_PURE(bool, Transport, device); }
+    void exchange(const std::vector<Message>& s, const std::vector<Message>& r, void* stream) override {
+        py::gil_scoped_acquire g;
+        py::function f = py::get_override(static_cast<const Transport*>(this), "exchange");
+        if (!f) throw Error("Transport.exchange not implemented");
+        py::list ls, lr;
+        for (auto& m : s) ls.append(py::make_tuple(m.peer, m.tag, (uintptr_t)m.ptr, m.bytes));
+        for (auto& m : r) lr.append(py::make_tuple(m.peer, m.tag, (uintptr_t)m.ptr, m.bytes));
+        f(ls, lr, (uintptr_t)stream);
+    }
+    void allreduce_max_u64(u64* data, size_t n, void* stream) override {
+        py::gil_scoped_acquire g;
+        py::function f = py::get_override(static_cast<const Transport*>(this), "allreduce_max_u64");
+        if (!f) throw Error("Transport.allreduce_max_u64 not implemented");
+        f((uintptr_t)data, n, (uintptr_t)stream);
+    }
+    void allreduce_max_host(double* data, size_t n) override {
+        py::gil_scoped_acquire g;
+        py::function f = py::get_override(static_cast<const Transport*>(this), "allreduce_max_host");
+        if (!f) throw Error("Transport.allreduce_max_host not implemented");
+        py::list v;
+        for (size_t q = 0; q < n; ++q) v.append(data[q]);
+        py::list out = f(v);
+        W3D_REQUIRE(out.size() == n, "allreduce_max_host returned a wrong length");
+        for (size_t q = 0; q < n; ++q) data[q] = out[q].cast<double>();
+    }
+    void barrier() override { PYBIND11_OVERRIDE_PURE(void, Transport, barrier); }
+};
+
+py::dict result_dict(const Config& c, const RunResult& r) {
+    py::dict d;
+    d["N"] = r.N;
+    d["timesteps"] = r.K;
+    d["nprocs"] = r.nprocs;
+    d["Np"] = r.Np;
+    d["dims"] = std::vector<int>{r.dims[0], r.dims[1], r.dims[2]};
+    d["dtype"] = dtype_name(r.dtype);
+    d["backend"] = r.backend;
+    d["kernel"] = r.kernel;
+    d["transport"] = r.transport;
+    d["courant"] = r.courant;
+    d["max_abs"] = r.max_abs;
+    d["max_rel"] = r.max_rel;
+    d["linf_abs"] = r.linf_final();
+    d["init_ms"] = r.t.init_ms;
+    d["total_ms"] = r.t.total_ms;
+    d["loop_ms"] = r.t.loop_ms;
+    d["exchange_ms"] = r.t.exchange_ms;
+    d["comm_ms"] = r.t.comm_ms;
+    d["error_ms"] = r.t.error_ms;
+    d["solve_ms"] = r.solve_ms;
+    d["mpts_per_s"] = r.mpts_per_s();
+    d["mpts_per_s_best"] = r.mpts_per_s_best();
+    d["aborted"] = r.aborted;
+    d["abort_layer"] = r.abort_layer;
+    d["abort_reason"] = r.abort_reason;
+    d["layers_done"] = r.layers_done;
+    d["resumed_from"] = r.resumed_from;
+    d["report"] = format_report(c, r);
+    d["output_file"] = output_filename(c, r);
+    d["json"] = json_summary(c, r);
+    return d;
+}
+
+py::dict run(const std::vector<std::string>& args, const std::string& backend,
+             Transport* transport, bool write, bool root) {
+    Config c = parse_cli(args);
+    RunResult r;
+    {
+        py::gil_scoped_release nogil;
+        if (backend == "cpu") r = run_cpu(c, transport);
+        else if (backend == "hip") r = run_hip(c, transport);
+        else throw Error("unknown backend " + backend);
+    }
+    if (write && root) write_report(c, r);
+    return result_dict(c, r);
+}
+
+template <class T>
+T* P(uintptr_t p) { return reinterpret_cast<T*>(p); }
+
+GridView gview(const std::vector<i64>& g) {
+    W3D_REQUIRE(g.size() == 5, "grid view = (nx, ny, nz, sj, si)");
+    GridView v;
+    v.nx = int(g[0]);
+    v.ny = int(g[1]);
+    v.nz = int(g[2]);
+    v.sj = int(g[3]);
+    v.si = g[4];
+    return v;
+}
+
+Box tobox(const std::vector<int>& b) {
+    W3D_REQUIRE(b.size() == 6, "box = (i0, i1, j0, j1, k0, k1)");
+    return Box{b[0], b[1], b[2], b[3], b[4], b[5]};
+}
+
+template <class T>
+void k_step(const std::string& kind, bool first, uintptr_t u1, uintptr_t u2, uintptr_t u,
+            const std::vector<i64>& g, const std::vector<std::vector<int>>& boxes, int ei0,
+            int ei1, const std::vector<int>& wrap, uintptr_t tx, uintptr_t ty, uintptr_t tz,
+            const std::vector<double>& coefs, uintptr_t err, int chunk, uintptr_t stream,
+            const std::vector<uintptr_t>& packbuf, const std::vector<int>& packidx) {
+    std::vector<Box> bx;
+    for (auto& b : boxes) bx.push_back(tobox(b));
+    Wrap w;
+    if (wrap.size() == 4) w.src[0] = wrap[0], w.dst[0] = wrap[1], w.src[1] = wrap[2], w.dst[1] = wrap[3];
+    FusedPack<T> fp;
+    if (packbuf.size() == 4 && packidx.size() == 4) {
+        fp.zbuf[0] = P<T>(packbuf[0]), fp.zbuf[1] = P<T>(packbuf[1]);
+        fp.ybuf[0] = P<T>(packbuf[2]), fp.ybuf[1] = P<T>(packbuf[3]);
+        fp.zk[0] = packidx[0], fp.zk[1] = packidx[1], fp.yj[0] = packidx[2], fp.yj[1] = packidx[3];
+    }
+    W3D_REQUIRE(coefs.size() == 5, "coefs = (hx2, hy2, hz2, coef, ct)");
+    StepCoefs c{coefs[0], coefs[1], coefs[2], coefs[3], coefs[4]};
+    launch_step<T>(kind == "naive" ? StepKernel::Naive : StepKernel::March, first, P<T>(u1),
+                   P<T>(u2), P<T>(u), gview(g), bx.data(), int(bx.size()), ei0, ei1, w, fp,
+                   P<T>(tx), P<T>(ty), P<T>(tz), c, P<u64>(err), chunk, (hipStream_t)stream);
+}
+
+template <class T>
+void k_init(uintptr_t u, const std::vector<i64>& g, const std::vector<int>& box,
+            const std::vector<int>& wrap, uintptr_t tx, uintptr_t ty, uintptr_t tz, double ct0,
+            uintptr_t err, uintptr_t stream) {
+    Wrap w;
+    if (wrap.size() == 4) w.src[0] = wrap[0], w.dst[0] = wrap[1], w.src[1] = wrap[2], w.dst[1] = wrap[3];
+    launch_init<T>(P<T>(u), gview(g), tobox(box), w, P<T>(tx), P<T>(ty), P<T>(tz), ct0,
+                   P<u64>(err), (hipStream_t)stream);
+}
+
+template <class T>
+void k_faces(uintptr_t u, const std::vector<i64>& g, const std::vector<std::tuple<uintptr_t, int, int>>& ops,
+             bool to_buf, uintptr_t stream) {
+    std::vector<FaceOp<T>> o;
+    for (auto& t : ops) o.push_back({P<T>(std::get<0>(t)), std::get<1>(t), std::get<2>(t)});
+    launch_faces<T>(P<T>(u), gview(g), o.data(), int(o.size()), to_buf, (hipStream_t)stream);
+}
+
+template <class T>
+void k_zero_faces(uintptr_t u, const std::vector<i64>& g, int mask, uintptr_t stream) {
+    launch_zero_faces<T>(P<T>(u), gview(g), mask, (hipStream_t)stream);
+}
+
+}  // namespace
+
+PYBIND11_MODULE(_wave3d_C, m) {
+    m.doc() = "wave3d native runtime (C++/HIP for MI355X)";
+    py::register_exception<Error>(m, "Wave3dError");
+
+    py::class_<Message>(m, "Message");
+    py::class_<Transport, PyTransport>(m, "Transport")
+        .def(py::init<>())
+        .def("name", &Transport::name)
+        .def("rank", &Transport::rank)
+        .def("size", &Transport::size)
+        .def("device", &Transport::device);
+
+    py::class_<RcclTransport, Transport>(m, "RcclTransport")
+        .def(py::init([](int rank, int size, py::bytes uid, int device) {
+                 std::string s = uid;
+                 py::gil_scoped_release nogil;
+                 return new RcclTransport(rank, size, s, device);
+             }),
+             py::arg("rank"), py::arg("size"), py::arg("uid"), py::arg("device"))
+        .def("barrier", [](RcclTransport& t) {
+            py::gil_scoped_release nogil;
+            t.barrier();
+        })
+        .def("check_async", &RcclTransport::check_async);
+    m.def("rccl_unique_id", []() { return py::bytes(rccl_unique_id()); });
+
+    py::class_<Session>(m, "Session", "Persistent solver: allocate once, solve() many times")
+        .def(py::init([](const std::vector<std::string>& args, const std::string& backend,
+                         Transport* tr) {
+                 Config c = parse_cli(args);
+                 py::gil_scoped_release nogil;
+                 if (backend == "cpu") return make_cpu_session(c, tr).release();
+                 if (backend == "hip") return make_hip_session(c, tr).release();
+                 throw Error("unknown backend " + backend);
+             }),
+             py::arg("args"), py::arg("backend") = "hip", py::arg("transport") = nullptr,
+             py::keep_alive<1, 4>())
+        .def("solve", [](Session& s, const std::vector<std::string>& args) {
+            Config c = parse_cli(args);
+            RunResult r;
+            {
+                py::gil_scoped_release nogil;
+                r = s.solve();
+            }
+            return result_dict(c, r);
+        }, py::arg("args"))
+        .def_property_readonly("init_ms", &Session::init_ms);
+
+    m.def("run", &run, py::arg("args"), py::arg("backend") = "hip",
+          py::arg("transport") = nullptr, py::arg("write") = true, py::arg("root") = true,
+          "Run the solver with reference-style CLI arguments; returns a result dict.");
+    m.def("parse", [](const std::vector<std::string>& a) {
+        Config c = parse_cli(a);
+        Problem p = Problem::from_config(c);
+        py::dict d;
+        d["N"] = c.N, d["Np"] = c.Np, d["T"] = c.T, d["timesteps"] = c.timesteps;
+        d["Lx"] = p.Lx, d["Ly"] = p.Ly, d["Lz"] = p.Lz, d["pi"] = p.pi;
+        d["a2"] = p.a2, d["a_t"] = p.a_t, d["tau"] = p.tau;
+        d["hx"] = p.hx, d["hy"] = p.hy, d["hz"] = p.hz;
+        d["coef"] = p.coef, d["coef_first"] = p.coef_first, d["courant"] = p.courant;
+        d["dtype"] = dtype_name(c.dtype), d["ranks"] = c.ranks, d["overlap"] = c.overlap;
+        d["kernel"] = c.kernel, d["chunk"] = c.chunk;
+        d["dims"] = std::vector<int>{c.dims[0], c.dims[1], c.dims[2]};
+        d["table_x"] = p.table_x(), d["table_y"] = p.table_y(), d["table_z"] = p.table_z();
+        d["table_t"] = p.table_t();
+        return d;
+    });
+    m.def("usage", &usage);
+    m.def("topology", [](int N, int nprocs, int rank, std::vector<int> dims) {
+        int d[3] = {0, 0, 0};
+        for (size_t q = 0; q < dims.size() && q < 3; ++q) d[q] = dims[q];
+        Topology t = Topology::make(N, nprocs, rank, d);
+        py::dict r;
+        r["dims"] = std::vector<int>{t.dims[0], t.dims[1], t.dims[2]};
+        r["coords"] = std::vector<int>{t.coords[0], t.coords[1], t.coords[2]};
+        r["ext"] = std::vector<int>{t.ext[0], t.ext[1], t.ext[2]};
+        r["off"] = std::vector<int>{t.off[0], t.off[1], t.off[2]};
+        r["nbr"] = std::vector<std::vector<int>>{{t.nbr[0][0], t.nbr[0][1]},
+                                                 {t.nbr[1][0], t.nbr[1][1]},
+                                                 {t.nbr[2][0], t.nbr[2][1]}};
+        auto bx = [](const Box& b) { return std::vector<int>{b.i0, b.i1, b.j0, b.j1, b.k0, b.k1}; };
+        r["compute_box"] = bx(t.compute_box());
+        r["error_box"] = bx(t.error_box());
+        r["owned_box"] = bx(t.owned_box());
+        HaloPlan hp = make_halo_plan(t, i64(t.ext[1] + 2) * (t.ext[2] + 2), t.ext[2] + 2);
+        auto msgs = [](const std::vector<FaceMsg>& v) {
+            py::list l;
+            for (auto& f : v) l.append(py::make_tuple(f.axis, f.side, f.peer, f.tag, f.count));
+            return l;
+        };
+        r["sends"] = msgs(hp.sends);
+        r["recvs"] = msgs(hp.recvs);
+        r["self_x"] = hp.self_x;
+        return r;
+    });
+    m.def("dims_create", [](int n, std::vector<int> dims) {
+        int d[3] = {0, 0, 0};
+        for (size_t q = 0; q < dims.size() && q < 3; ++q) d[q] = dims[q];
+        Topology::dims_create(n, d);
+        return std::vector<int>{d[0], d[1], d[2]};
+    });
+    m.def("encode_max_key", &encode_max_key);
+    m.def("decode_max_key", &decode_max_key);
+    m.def("march_rows_per_thread", &march_rows_per_thread);
+
+    // kernel-level entry points (device pointers as ints, explicit stream)
+    m.def("k_step_f64", &k_step<double>);
+    m.def("k_step_f32", &k_step<float>);
+    m.def("k_init_f64", &k_init<double>);
+    m.def("k_init_f32", &k_init<float>);
+    m.def("k_faces_f64", &k_faces<double>);
+    m.def("k_faces_f32", &k_faces<float>);
+    m.def("k_zero_faces_f64", &k_zero_faces<double>);
+    m.def("k_zero_faces_f32", &k_zero_faces<float>);
+    m.def("k_init_err", [](uintptr_t err, int layers, uintptr_t s) {
+        launch_init_err(P<u64>(err), layers, (hipStream_t)s);
+    });
+    m.def("k_encode_keys", [](uintptr_t v, uintptr_t k, int n, uintptr_t s) {
+        launch_encode_keys(P<double>(v), P<u64>(k), n, (hipStream_t)s);
+    });
+    m.def("device_count", []() {
+        int n = 0;
+        if (hipGetDeviceCount(&n) != hipSuccess) n = 0;
+        return n;
+    });
+}

@@ -1,0 +1,63 @@
+// Command-line / run configuration.
+//
+// Positional part is identical to every reference program (C03):
+//   prog N Np Lx Ly Lz [T=1] [timesteps=20]      (mpi_new.cpp:382-393, cuda_sol.cpp:453-464)
+// `Lx|Ly|Lz` accept the literal `pi`. Long flags may follow the positionals.
+#pragma once
+
+#include <string>
+#include <vector>
+
+#include "common.hpp"
+
+namespace wave3d {
+
+enum class PiMode { Ref, Exact };      // truncated 3.1415926535 (CPU variants) vs full precision
+enum class ICMode { Ref, Shifted };    // sin(2πx/Lx) vs sin(2πx/Lx + 0.7)
+enum class ReportFormat { New, Omp, Cuda, None };
+
+struct Config {
+    // positionals
+    int N = 32;
+    int Np = 1;
+    double Lx = 0, Ly = 0, Lz = 0;
+    double T = 1.0;
+    int timesteps = 20;
+    bool Lx_is_pi = false, Ly_is_pi = false, Lz_is_pi = false;
+
+    // extensions
+    DType dtype = DType::F64;
+    PiMode pi = PiMode::Ref;
+    ICMode ic = ICMode::Ref;
+    int dims[3] = {0, 0, 0};        // 0 = let dims_create choose (MPI_Dims_create semantics)
+    bool overlap = true;            // interior/shell split with comm on a second stream
+    bool json = false;              // one-line JSON summary on stdout (rank 0)
+    int check_every = 0;            // >0: abort early when a layer's error is NaN/Inf/>1
+    bool strict_cfl = false;        // refuse C > 1/sqrt(3)
+    std::string transport = "auto"; // auto | rccl | loopback
+    int ranks = 0;                  // >0: number of logical ranks simulated in-process
+    ReportFormat format = ReportFormat::New;
+    std::string out_dir = ".";
+    std::string out_name;           // override of output_N{N}_Np{Np}.txt
+    bool quiet = false;
+    int checkpoint_every = 0;
+    std::string checkpoint_dir;
+    std::string resume_dir;
+    std::string kernel = "auto";    // auto | march | naive | tb2
+    int chunk = 0;                  // i-planes per marching work item (0 = auto)
+    int repeat = 1;                 // timed solves (benchmark mode)
+    int warmup = 0;                 // untimed solves before the timed ones
+    bool profile = false;           // per-phase hipEvent timers
+    std::string fault;              // fault injection spec, e.g. "drop_face:1:5" (or env WAVE_FI)
+    int device = -1;                // explicit device id (default: local rank)
+    int threads = 0;                // CPU backend OpenMP threads (0 = Np)
+    bool print_layers = false;      // "calculating layer n" lines (reference stdout)
+};
+
+// Parse argv; throws wave3d::Error with a usage message on malformed input.
+Config parse_cli(int argc, const char* const* argv);
+Config parse_cli(const std::vector<std::string>& args);  // args without argv[0]
+
+std::string usage();
+
+}  // namespace wave3d

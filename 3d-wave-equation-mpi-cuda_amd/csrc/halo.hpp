@@ -1,0 +1,69 @@
+// Face-halo exchange plan and the transport interface (P6).
+//
+// Each rank sends the owned plane next to each existing neighbour and receives into the
+// ghost plane on that side. Tags follow the reference (mpi_new.cpp:201-238): a message
+// travelling towards +axis carries tag 2a+1, towards -axis tag 2a+2. Sends and receives
+// are listed in one canonical order (axis, then tag), so transports without tags (RCCL)
+// match messages by per-peer FIFO order.
+//
+// Payloads are contiguous:
+//   x: the whole padded (j,k) plane — already contiguous in the [i][j][k] layout, sent and
+//      received in place, no pack/unpack;
+//   y: rows i=1..X of the (i,k) face, k over the full padded row -> X*pitch elements;
+//   z: i=1..X, j=0..Y+1 of the (i,j) face                       -> X*(Y+2) elements.
+// A rank that is its own x-neighbour (dims[0] == 1) wraps locally instead of messaging.
+#pragma once
+
+#include <string>
+#include <vector>
+
+#include "common.hpp"
+#include "topology.hpp"
+
+namespace wave3d {
+
+struct FaceMsg {
+    int axis = 0;
+    int side = 0;   // 0 = minus face, 1 = plus face of *this* rank
+    int peer = -1;
+    int tag = 0;
+    i64 count = 0;  // elements
+};
+
+struct HaloPlan {
+    std::vector<FaceMsg> sends;  // canonical order
+    std::vector<FaceMsg> recvs;  // canonical order
+    bool self_x = false;         // periodic x neighbour is this rank
+};
+
+// `x_plane` = elements of one padded (j,k) plane, `row` = elements of a y-face row.
+HaloPlan make_halo_plan(const Topology& t, i64 x_plane, int row);
+
+// Description of one message for a transport.
+struct Message {
+    int peer = -1;
+    int tag = 0;
+    void* ptr = nullptr;
+    size_t bytes = 0;
+};
+
+// A transport moves the messages of one exchange. Device transports order the operation
+// on `stream` (a hipStream_t) and return without host synchronisation; host transports
+// complete before returning.
+class Transport {
+public:
+    virtual ~Transport() = default;
+    virtual std::string name() const = 0;
+    virtual int rank() const = 0;
+    virtual int size() const = 0;
+    virtual bool device() const = 0;
+    virtual void exchange(const std::vector<Message>& sends, const std::vector<Message>& recvs,
+                          void* stream) = 0;
+    // In-place max over ranks of n order-preserving error keys (see encode_max_key).
+    virtual void allreduce_max_u64(u64* data, size_t n, void* stream) = 0;
+    // Host doubles, max over ranks (timers).
+    virtual void allreduce_max_host(double* data, size_t n) = 0;
+    virtual void barrier() = 0;
+};
+
+}  // namespace wave3d

@@ -1,0 +1,521 @@
+// Hand-written CDNA4 (gfx950) kernels of the wave3d solver.
+//
+// Replaces the reference's CUDA kernels (cuda_sol_kernels.cu): calculate_layer (:24-47),
+// layer0 (:179-190), layer1 (:192-213), prepare_layer (:230-268), calculate_max_errors
+// (:50-89), copy_to_matrices / copy_to_grid (:91-177) — with a different design:
+//
+//  * k_march: 2.5-D blocked leapfrog. A 256-thread workgroup (4 wave64s) owns a
+//    16(j) x 64(k) tile of the (j,k) plane and marches along i. Each lane keeps its
+//    4-row column strip for planes i-1, i, i+1 (and i+2 in flight) in registers, the
+//    current plane is staged in a double-buffered LDS tile (one barrier per plane) for the
+//    j±1 / k±1 neighbours, so u^{n-1} is read from HBM once and u^{n-2} once per point.
+//    The analytic error is fused (separable tables, no transcendentals), reduced per
+//    workgroup with wave shuffles and committed with one 64-bit atomicMax per slot —
+//    no per-point error arrays, no memsets, no host syncs (cuda_sol.cpp:395-418).
+//  * The periodic x wrap (dims[0] == 1) and the y/z halo packing can be fused into the
+//    stores, so a single-GPU step is exactly one launch.
+//  * 64-bit plane offsets (the reference's int indexing overflows, Appendix B7).
+//
+// FP contraction is off in this file (-ffp-contract=off + pragmas in stencil_math.hpp):
+// every value is rounded exactly like the reference CPU programs, so the reported errors
+// are bitwise those of mpi_new.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+
+#include "hip_kernels.hpp"
+#include "stencil_math.hpp"
+
+#define HIP_OK(x)                                                                      \
+    do {                                                                               \
+        hipError_t e_ = (x);                                                           \
+        if (e_ != hipSuccess)                                                          \
+            throw ::wave3d::Error(std::string("HIP error ") + hipGetErrorString(e_) + \
+                                  " at " __FILE__ ":" + std::to_string(__LINE__));     \
+    } while (0)
+
+namespace wave3d {
+namespace {
+
+constexpr int kThreads = 256;
+constexpr int kWaves = kThreads / 64;
+constexpr int kRows = 4;                 // rows per lane in k_march
+constexpr int kTJ = kWaves * kRows;      // tile rows (j)
+constexpr int kTK = 64;                  // tile columns (k) = one wave64
+constexpr int kLW = kTK + 2;             // LDS row incl. k halos
+constexpr int kNaiveTJ = kWaves;         // naive kernel: one row per wave
+
+struct BoxLaunch {
+    int i0, i1, j0, j1, k0, k1;
+    int kbase;     // k of lane 0 of the first tile (aligned to 1 + 64t)
+    int tiles_k, tiles_j, chunk;
+    int block_begin;
+};
+
+template <class T>
+struct StepParams {
+    const T* u1;
+    const T* u2;
+    T* u;
+    i64 si;
+    int sj;
+    int jmax, kmax;  // largest valid j / k index in storage (ny-1, nz-1)
+    int nbox;
+    BoxLaunch box[kMaxBoxes];
+    int ei0, ei1;
+    int wsrc0, wdst0, wsrc1, wdst1;
+    T* zbuf0;
+    T* zbuf1;
+    int zk0, zk1;
+    T* ybuf0;
+    T* ybuf1;
+    int yj0, yj1;
+    int zrow, yrow;  // packed row lengths (Y+2, Z+2)
+    const T* tx;
+    const T* ty;
+    const T* tz;
+    T hx2, hy2, hz2, coef, ct;
+    u64* err;
+};
+
+__device__ __forceinline__ u64 enc_key(double d) {
+    u64 b = (u64)__double_as_longlong(d);
+    return (b >> 63) ? ~b : (b | 0x8000000000000000ull);
+}
+
+template <class T>
+__device__ __forceinline__ T wave_max(T v) {
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+        T o = __shfl_xor(v, off, 64);
+        v = o > v ? o : v;
+    }
+    return v;
+}
+
+// Workgroup reduction of the running maxima + one atomic per slot (race-free, no
+// divergent barrier: every thread reaches the __syncthreads, cf. Appendix B5).
+template <class T>
+__device__ __forceinline__ void commit_errors(T ma, T mr, bool bad, u64* err) {
+    __shared__ double red[2][kWaves];
+    __shared__ int redb[kWaves];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    ma = wave_max(ma);
+    mr = wave_max(mr);
+    unsigned long long any = __ballot(bad);
+    if (lane == 0) {
+        red[0][w] = double(ma);
+        red[1][w] = double(mr);
+        redb[w] = any != 0ull;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double a = red[0][0], r = red[1][0];
+        int b = redb[0];
+#pragma unroll
+        for (int q = 1; q < kWaves; ++q) {
+            if (red[0][q] > a) a = red[0][q];
+            if (red[1][q] > r) r = red[1][q];
+            b |= redb[q];
+        }
+        atomicMax(err + 0, enc_key(a));
+        atomicMax(err + 1, enc_key(r));
+        if (b) atomicMax(err + 2, 1ull);
+    }
+}
+
+template <class T>
+__device__ __forceinline__ int find_box(const StepParams<T>& p, int bid) {
+    int b = 0;
+#pragma unroll
+    for (int q = 1; q < kMaxBoxes; ++q)
+        if (q < p.nbox && bid >= p.box[q].block_begin) b = q;
+    return b;
+}
+
+template <class T>
+__device__ __forceinline__ void store_point(const StepParams<T>& p, int i, int j, int k, i64 o,
+                                            int rowoff, T v) {
+    p.u[o] = v;
+    if (i == p.wsrc0) p.u[i64(p.wdst0) * p.si + rowoff] = v;
+    if (i == p.wsrc1) p.u[i64(p.wdst1) * p.si + rowoff] = v;
+    if (k == p.zk0) p.zbuf0[i64(i - 1) * p.zrow + j] = v;
+    if (k == p.zk1) p.zbuf1[i64(i - 1) * p.zrow + j] = v;
+    if (j == p.yj0) p.ybuf0[i64(i - 1) * p.yrow + k] = v;
+    if (j == p.yj1) p.ybuf1[i64(i - 1) * p.yrow + k] = v;
+}
+
+// ---------------------------------------------------------------------------------------
+// 2.5-D marching kernel (LDS tile + register-rolling i column).
+template <class T, bool FIRST>
+__global__ void __launch_bounds__(kThreads) k_march(const StepParams<T> p) {
+    __shared__ T lds[2][kTJ + 2][kLW];
+
+    const int bid = blockIdx.x;
+    const int b = find_box(p, bid);
+    const BoxLaunch B = p.box[b];
+    int local = bid - B.block_begin;
+    const int tk = local % B.tiles_k;
+    local /= B.tiles_k;
+    const int tj = local % B.tiles_j;
+    const int ci = local / B.tiles_j;
+
+    const int lane = threadIdx.x & 63;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int kb = B.kbase + tk * kTK;
+    const int k = kb + lane;
+    const int jt = B.j0 + tj * kTJ;
+    const int ib = B.i0 + ci * B.chunk;
+    const int ie = min(B.i1, ib + B.chunk - 1);
+
+    const bool kload = k <= p.kmax;
+    const bool kin = k >= B.k0 && k <= B.k1;
+    const i64 si = p.si;
+
+    int rowoff[kRows];
+    bool ld_ok[kRows], valid[kRows];
+    T ty[kRows];
+#pragma unroll
+    for (int r = 0; r < kRows; ++r) {
+        const int j = jt + w * kRows + r;
+        rowoff[r] = j * p.sj + k;
+        ld_ok[r] = kload && j <= p.jmax;
+        valid[r] = kin && j <= B.j1;
+        ty[r] = valid[r] ? p.ty[j] : T(0);
+    }
+    const T tz = kin ? p.tz[k] : T(0);
+
+    // halo role of this lane: one LDS cell per plane
+    int hoff = 0, hrow = 0, hcol = 0;
+    bool hon = false;
+    if (w == 0) {  // row jt-1
+        hon = kload;
+        hoff = (jt - 1) * p.sj + k;
+        hrow = 0;
+        hcol = 1 + lane;
+    } else if (w == kWaves - 1) {  // row jt+TJ
+        const int j = jt + kTJ;
+        hon = kload && j <= p.jmax;
+        hoff = j * p.sj + k;
+        hrow = kTJ + 1;
+        hcol = 1 + lane;
+    } else if (w == 1) {  // columns kb-1 (lanes 0..TJ-1) and kb+64 (lanes 32..32+TJ-1)
+        const int side = lane >> 5, rr = lane & 31;
+        const int j = jt + rr;
+        const int kk = side ? kb + kTK : kb - 1;
+        hon = rr < kTJ && j <= p.jmax && kk <= p.kmax;
+        hoff = j * p.sj + kk;
+        hrow = 1 + rr;
+        hcol = side ? kTK + 1 : 0;
+    }
+
+    const T* __restrict__ u1 = p.u1;
+    const T* __restrict__ u2 = p.u2;
+
+    T Pv[kRows], Cv[kRows], Nv[kRows], U2c[kRows];
+#pragma unroll
+    for (int r = 0; r < kRows; ++r) {
+        Pv[r] = ld_ok[r] ? u1[i64(ib - 1) * si + rowoff[r]] : T(0);
+        Cv[r] = ld_ok[r] ? u1[i64(ib) * si + rowoff[r]] : T(0);
+        Nv[r] = ld_ok[r] ? u1[i64(ib + 1) * si + rowoff[r]] : T(0);
+        U2c[r] = (!FIRST && valid[r]) ? u2[i64(ib) * si + rowoff[r]] : T(0);
+    }
+    T H = hon ? u1[i64(ib) * si + hoff] : T(0);
+
+    T ma = T(kErrInit), mr = T(kErrInit);
+    bool bad = false;
+    int buf = 0;
+    for (int i = ib; i <= ie; ++i) {
+        // prefetch plane i+2 (own rows), plane i+1 (halo, u2)
+        T NN[kRows], U2n[kRows], Hn = T(0);
+        const bool more = i < ie;
+#pragma unroll
+        for (int r = 0; r < kRows; ++r) {
+            NN[r] = (more && ld_ok[r]) ? u1[i64(i + 2) * si + rowoff[r]] : T(0);
+            U2n[r] = (!FIRST && more && valid[r]) ? u2[i64(i + 1) * si + rowoff[r]] : T(0);
+        }
+        if (more && hon) Hn = u1[i64(i + 1) * si + hoff];
+
+        // stage plane i
+#pragma unroll
+        for (int r = 0; r < kRows; ++r) lds[buf][1 + w * kRows + r][1 + lane] = Cv[r];
+        if (hon) lds[buf][hrow][hcol] = H;
+        __syncthreads();
+
+        const T sx = p.tx[i];
+        const bool erow = i >= p.ei0 && i <= p.ei1;
+#pragma unroll
+        for (int r = 0; r < kRows; ++r) {
+            const int lr = 1 + w * kRows + r;
+            const T jm = r == 0 ? lds[buf][lr - 1][1 + lane] : Cv[r - 1];
+            const T jp = r == kRows - 1 ? lds[buf][lr + 1][1 + lane] : Cv[r + 1];
+            const T km = lds[buf][lr][lane];
+            const T kp = lds[buf][lr][lane + 2];
+            const T lap = laplace7(Cv[r], Pv[r], Nv[r], jm, jp, km, kp, p.hx2, p.hy2, p.hz2);
+            const T v = FIRST ? taylor_first(Cv[r], lap, p.coef) : leapfrog(Cv[r], U2c[r], lap, p.coef);
+            if (valid[r]) {
+                const int j = jt + w * kRows + r;
+                store_point(p, i, j, k, i64(i) * si + rowoff[r], rowoff[r], v);
+                bad |= nonfinite(v);
+                if (erow) accumulate_error(v, analytic(sx, ty[r], tz, p.ct), ma, mr);
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < kRows; ++r) {
+            Pv[r] = Cv[r];
+            Cv[r] = Nv[r];
+            Nv[r] = NN[r];
+            U2c[r] = U2n[r];
+        }
+        H = Hn;
+        buf ^= 1;
+    }
+    commit_errors(ma, mr, bad, p.err);
+}
+
+// ---------------------------------------------------------------------------------------
+// One-point-per-lane reference kernel (7 neighbour loads through L1/L2). Kept for
+// ablation (profiles/) and as a second, independent device implementation.
+template <class T, bool FIRST>
+__global__ void __launch_bounds__(kThreads) k_naive(const StepParams<T> p) {
+    const int bid = blockIdx.x;
+    const int b = find_box(p, bid);
+    const BoxLaunch B = p.box[b];
+    int local = bid - B.block_begin;
+    const int tk = local % B.tiles_k;
+    local /= B.tiles_k;
+    const int tj = local % B.tiles_j;
+    const int i = B.i0 + local / B.tiles_j;  // chunk == 1
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int k = B.kbase + tk * kTK + lane;
+    const int j = B.j0 + tj * kNaiveTJ + w;
+    T ma = T(kErrInit), mr = T(kErrInit);
+    bool bad = false;
+    if (k >= B.k0 && k <= B.k1 && j <= B.j1) {
+        const i64 si = p.si;
+        const int rowoff = j * p.sj + k;
+        const i64 o = i64(i) * si + rowoff;
+        const T c = p.u1[o];
+        const T lap = laplace7(c, p.u1[o - si], p.u1[o + si], p.u1[o - p.sj], p.u1[o + p.sj],
+                               p.u1[o - 1], p.u1[o + 1], p.hx2, p.hy2, p.hz2);
+        const T v = FIRST ? taylor_first(c, lap, p.coef) : leapfrog(c, p.u2[o], lap, p.coef);
+        store_point(p, i, j, k, o, rowoff, v);
+        bad = nonfinite(v);
+        if (i >= p.ei0 && i <= p.ei1)
+            accumulate_error(v, analytic(p.tx[i], p.ty[j], p.tz[k], p.ct), ma, mr);
+    }
+    commit_errors(ma, mr, bad, p.err);
+}
+
+// ---------------------------------------------------------------------------------------
+template <class T>
+__global__ void __launch_bounds__(kThreads) k_init(T* u, i64 si, int sj, Box bx, int ws0,
+                                                   int wd0, int ws1, int wd1, const T* tx,
+                                                   const T* ty, const T* tz, T ct, u64* err) {
+    const int k = bx.k0 + blockIdx.x * 64 + (threadIdx.x & 63);
+    const int j = bx.j0 + blockIdx.y * kWaves + (threadIdx.x >> 6);
+    const int i = bx.i0 + blockIdx.z;
+    T ma = T(kErrInit), mr = T(kErrInit);
+    bool bad = false;
+    if (k <= bx.k1 && j <= bx.j1) {
+        const int rowoff = j * sj + k;
+        const T f = analytic(tx[i], ty[j], tz[k], ct);
+        u[i64(i) * si + rowoff] = f;
+        if (i == ws0) u[i64(wd0) * si + rowoff] = f;
+        if (i == ws1) u[i64(wd1) * si + rowoff] = f;
+        bad = nonfinite(f);
+        accumulate_error(f, analytic(tx[i], ty[j], tz[k], ct), ma, mr);
+    }
+    commit_errors(ma, mr, bad, err);
+}
+
+template <class T>
+__global__ void k_zero_faces(T* u, i64 si, int sj, int X, int Y, int Z, int mask) {
+    const int i = 1 + blockIdx.y;
+    const int t = 1 + blockIdx.x * blockDim.x + threadIdx.x;
+    T* pl = u + i64(i) * si;
+    if (t <= Y) {
+        if (mask & 1) pl[t * sj + 1] = T(0);
+        if (mask & 2) pl[t * sj + Z] = T(0);
+    }
+    if (t <= Z) {
+        if (mask & 4) pl[1 * sj + t] = T(0);
+        if (mask & 8) pl[Y * sj + t] = T(0);
+    }
+}
+
+template <class T>
+struct FaceOps {
+    FaceOp<T> op[4];
+};
+
+template <class T>
+__global__ void k_faces(T* u, i64 si, int sj, int ny, int nz, FaceOps<T> ops, bool to_buf) {
+    const FaceOp<T> f = ops.op[blockIdx.z];
+    const int i = 1 + blockIdx.y;
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    const int len = f.axis == 1 ? nz : ny;
+    if (t >= len) return;
+    T* g = f.axis == 1 ? u + i64(i) * si + i64(f.index) * sj + t
+                       : u + i64(i) * si + i64(t) * sj + f.index;
+    T* q = f.buf + i64(i - 1) * len + t;
+    if (to_buf) *q = *g;
+    else *g = *q;
+}
+
+__global__ void k_init_err(u64* err, int n) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t < n) err[t] = (t % 3 == 2) ? 0ull : enc_key(kErrInit);
+}
+
+__global__ void k_encode(const double* v, u64* k, int n) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t < n) k[t] = enc_key(v[t]);
+}
+
+inline int cdiv(int a, int b) { return (a + b - 1) / b; }
+
+}  // namespace
+
+int march_rows_per_thread() { return kRows; }
+
+template <class T>
+void launch_step(StepKernel kind, bool first, const T* u1, const T* u2, T* u, const GridView& gv,
+                 const Box* boxes, int nbox, int ei0, int ei1, const Wrap& wrap,
+                 const FusedPack<T>& pack, const T* tx, const T* ty, const T* tz,
+                 const StepCoefs& c, u64* err, int chunk, hipStream_t s) {
+    W3D_REQUIRE(nbox >= 1 && nbox <= kMaxBoxes, "bad box count");
+    StepParams<T> p{};
+    p.u1 = u1;
+    p.u2 = u2;
+    p.u = u;
+    p.si = gv.si;
+    p.sj = gv.sj;
+    p.jmax = gv.ny - 1;
+    p.kmax = gv.nz - 1;
+    p.ei0 = ei0;
+    p.ei1 = ei1;
+    p.wsrc0 = wrap.src[0];
+    p.wdst0 = wrap.dst[0];
+    p.wsrc1 = wrap.src[1];
+    p.wdst1 = wrap.dst[1];
+    p.zbuf0 = pack.zbuf[0];
+    p.zbuf1 = pack.zbuf[1];
+    p.zk0 = pack.zbuf[0] ? pack.zk[0] : -7;
+    p.zk1 = pack.zbuf[1] ? pack.zk[1] : -7;
+    p.ybuf0 = pack.ybuf[0];
+    p.ybuf1 = pack.ybuf[1];
+    p.yj0 = pack.ybuf[0] ? pack.yj[0] : -7;
+    p.yj1 = pack.ybuf[1] ? pack.yj[1] : -7;
+    p.zrow = gv.ny;
+    p.yrow = gv.nz;
+    p.tx = tx;
+    p.ty = ty;
+    p.tz = tz;
+    p.hx2 = T(c.hx2);
+    p.hy2 = T(c.hy2);
+    p.hz2 = T(c.hz2);
+    p.coef = T(c.coef);
+    p.ct = T(c.ct);
+    p.err = err;
+    const bool march = kind == StepKernel::March;
+    const int tj_rows = march ? kTJ : kNaiveTJ;
+    int nb = 0, total = 0;
+    for (int q = 0; q < nbox; ++q) {
+        const Box& bx = boxes[q];
+        if (bx.empty()) continue;
+        W3D_REQUIRE(bx.i0 >= 1 && bx.i1 <= gv.nx - 2 && bx.j0 >= 1 && bx.j1 <= gv.ny - 2 &&
+                        bx.k0 >= 1 && bx.k1 <= gv.nz - 2,
+                    "step box outside the owned region");
+        BoxLaunch& L = p.box[nb];
+        L.i0 = bx.i0, L.i1 = bx.i1, L.j0 = bx.j0, L.j1 = bx.j1, L.k0 = bx.k0, L.k1 = bx.k1;
+        const int t0 = (bx.k0 - 1) / kTK, t1 = (bx.k1 - 1) / kTK;
+        L.kbase = 1 + t0 * kTK;
+        L.tiles_k = t1 - t0 + 1;
+        L.tiles_j = cdiv(bx.j1 - bx.j0 + 1, tj_rows);
+        const int planes = bx.i1 - bx.i0 + 1;
+        int ch = 1;
+        if (march) {
+            if (chunk > 0) {
+                ch = std::min(chunk, planes);
+            } else {
+                // aim at ~2 resident waves of workgroups over the 256 CUs
+                const int tiles = L.tiles_k * L.tiles_j;
+                const int want = std::max(1, 2048 / std::max(1, tiles));
+                ch = std::max(8, cdiv(planes, want));
+                ch = std::min(ch, planes);
+            }
+        }
+        L.chunk = ch;
+        L.block_begin = total;
+        total += L.tiles_k * L.tiles_j * cdiv(planes, ch);
+        ++nb;
+    }
+    p.nbox = nb;
+    if (nb == 0) return;
+    void (*kern)(const StepParams<T>);
+    if (march) kern = first ? k_march<T, true> : k_march<T, false>;
+    else kern = first ? k_naive<T, true> : k_naive<T, false>;
+    hipLaunchKernelGGL(kern, dim3(total), dim3(kThreads), 0, s, p);
+    HIP_OK(hipGetLastError());
+}
+
+template <class T>
+void launch_init(T* u, const GridView& gv, const Box& bx, const Wrap& wrap, const T* tx,
+                 const T* ty, const T* tz, double ct0, u64* err, hipStream_t s) {
+    if (bx.empty()) return;
+    W3D_REQUIRE(bx.i0 >= 1 && bx.i1 <= gv.nx - 2 && bx.j1 <= gv.ny - 2 && bx.k1 <= gv.nz - 2,
+                "init box outside the owned region");
+    dim3 grid(cdiv(bx.k1 - bx.k0 + 1, 64), cdiv(bx.j1 - bx.j0 + 1, kWaves), bx.i1 - bx.i0 + 1);
+    hipLaunchKernelGGL(k_init<T>, grid, dim3(kThreads), 0, s, u, gv.si, gv.sj, bx, wrap.src[0],
+                       wrap.dst[0], wrap.src[1], wrap.dst[1], tx, ty, tz, T(ct0), err);
+    HIP_OK(hipGetLastError());
+}
+
+template <class T>
+void launch_zero_faces(T* u, const GridView& gv, int mask, hipStream_t s) {
+    if (!mask) return;
+    const int X = gv.nx - 2, Y = gv.ny - 2, Z = gv.nz - 2;
+    dim3 grid(cdiv(std::max(Y, Z), 256), X);
+    hipLaunchKernelGGL(k_zero_faces<T>, grid, dim3(256), 0, s, u, gv.si, gv.sj, X, Y, Z, mask);
+    HIP_OK(hipGetLastError());
+}
+
+template <class T>
+void launch_faces(T* u, const GridView& gv, const FaceOp<T>* ops, int nops, bool to_buf,
+                  hipStream_t s) {
+    W3D_REQUIRE(nops <= 4, "too many faces");
+    if (nops <= 0) return;
+    FaceOps<T> f{};
+    for (int q = 0; q < nops; ++q) f.op[q] = ops[q];
+    const int len = std::max(gv.ny, gv.nz);
+    dim3 grid(cdiv(len, 256), gv.nx - 2, nops);
+    hipLaunchKernelGGL(k_faces<T>, grid, dim3(256), 0, s, u, gv.si, gv.sj, gv.ny, gv.nz, f,
+                       to_buf);
+    HIP_OK(hipGetLastError());
+}
+
+void launch_init_err(u64* err, int layers, hipStream_t s) {
+    const int n = layers * 3;
+    hipLaunchKernelGGL(k_init_err, dim3(cdiv(n, 256)), dim3(256), 0, s, err, n);
+    HIP_OK(hipGetLastError());
+}
+
+void launch_encode_keys(const double* v, u64* k, int n, hipStream_t s) {
+    hipLaunchKernelGGL(k_encode, dim3(cdiv(n, 256)), dim3(256), 0, s, v, k, n);
+    HIP_OK(hipGetLastError());
+}
+
+#define W3D_INST(T)                                                                          \
+    template void launch_step<T>(StepKernel, bool, const T*, const T*, T*, const GridView&,  \
+                                 const Box*, int, int, int, const Wrap&, const FusedPack<T>&, \
+                                 const T*, const T*, const T*, const StepCoefs&, u64*, int,   \
+                                 hipStream_t);                                               \
+    template void launch_init<T>(T*, const GridView&, const Box&, const Wrap&, const T*,     \
+                                 const T*, const T*, double, u64*, hipStream_t);             \
+    template void launch_zero_faces<T>(T*, const GridView&, int, hipStream_t);               \
+    template void launch_faces<T>(T*, const GridView&, const FaceOp<T>*, int, bool, hipStream_t);
+W3D_INST(double)
+W3D_INST(float)
+
+}  // namespace wave3d

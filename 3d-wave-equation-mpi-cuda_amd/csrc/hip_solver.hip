@@ -1,0 +1,614 @@
+// MI355X solver driver (replaces cuda_sol.cpp's calculate_num_sol/exchange, §3.3-3.4).
+//
+// Execution model per time layer n (one process per GPU, device transport):
+//   compute stream : [zero Dirichlet faces, n<=3] -> interior(n) -> wait halo(n-1)
+//                    -> shell(n) (+ fused y/z face packing) -> record layer(n)
+//   comm stream    : wait layer(n) -> transport send/recv (x planes in place, packed y/z)
+//                    -> unpack y/z ghosts -> record halo(n)
+// so the RCCL exchange of layer n overlaps the interior of layer n+1. No host
+// synchronisation inside the time loop (the reference syncs >= 4x per layer); errors stay
+// in per-layer device slots until one max-allreduce at the end.
+// Single GPU (dims 1x1x1): one launch per layer, the periodic wrap fused into the stores.
+// In-process ranks (--ranks P): P subdomains on this GPU, one stream, D2D loopback copies.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cstring>
+#include <iostream>
+#include <memory>
+
+#include "checkpoint.hpp"
+#include "hip_kernels.hpp"
+#include "problem.hpp"
+#include "solver.hpp"
+
+#define HIP_CHECK(x)                                                                   \
+    do {                                                                               \
+        hipError_t e_ = (x);                                                           \
+        if (e_ != hipSuccess)                                                          \
+            throw ::wave3d::Error(std::string("HIP error ") + hipGetErrorString(e_) + \
+                                  " at " __FILE__ ":" + std::to_string(__LINE__));     \
+    } while (0)
+
+namespace wave3d {
+namespace {
+
+using clk = std::chrono::steady_clock;
+
+template <class T>
+struct DevRank {
+    Topology topo;
+    GridView gv;
+    int lead = 0;
+    T* alloc[3] = {nullptr, nullptr, nullptr};
+    T* g[3] = {nullptr, nullptr, nullptr};
+    T *tx = nullptr, *ty = nullptr, *tz = nullptr;
+    HaloPlan plan;
+    std::vector<T*> sbuf, rbuf;  // y/z messages only (x messages live in the grid)
+    u64* err = nullptr;          // (K+1) * kSlotsPerLayer
+    Box compute, error, owned, interior;
+    std::vector<Box> shell;
+    int zero_mask = 0;
+    Wrap wrap;
+    FusedPack<T> pack;           // pointers into sbuf
+};
+
+template <class T>
+class HipSolver {
+public:
+    HipSolver(const Config& c, Transport* ext) : cfg_(c), ext_(ext) {
+        prob_ = Problem::from_config(c);
+        fault_ = FaultSpec::parse(c.fault);
+        if (ext_) {
+            W3D_REQUIRE(ext_->device(), "run_hip needs a device transport");
+            world_ = ext_->size();
+            local_ = {ext_->rank()};
+        } else {
+            world_ = std::max(1, c.ranks);
+            for (int r = 0; r < world_; ++r) local_.push_back(r);
+        }
+        if (c.kernel == "naive") kind_ = StepKernel::Naive;
+        else if (c.kernel == "auto" || c.kernel == "march") kind_ = StepKernel::March;
+        else throw Error("wave3d: unknown --kernel " + c.kernel);
+        // interior/shell split + comm stream whenever there is a remote halo to hide
+        overlap_ = c.overlap && (ext_ != nullptr || world_ > 1);
+    }
+
+    ~HipSolver() { release(); }
+
+    void init() {
+        auto t0 = clk::now();
+        setup();
+        HIP_CHECK(hipDeviceSynchronize());
+        init_ms_ = std::chrono::duration<double, std::milli>(clk::now() - t0).count();
+    }
+
+    double init_ms() const { return init_ms_; }
+
+    RunResult solve_one() {
+        RunResult res;
+        res.N = prob_.N;
+        res.K = prob_.K;
+        res.nprocs = world_;
+        res.Np = world_;
+        res.dtype = cfg_.dtype;
+        res.backend = "hip";
+        res.kernel = kind_ == StepKernel::March ? "march" : "naive";
+        res.courant = prob_.courant;
+        res.transport = ext_ ? ext_->name() : (world_ > 1 ? "loopback" : "self");
+        for (int a = 0; a < 3; ++a) res.dims[a] = ranks_[0].topo.dims[a];
+        Timings t;
+        solve(res, t);
+        t.init_ms = init_ms_;
+        double tv[5] = {t.total_ms, t.loop_ms, t.exchange_ms, t.comm_ms, t.error_ms};
+        if (ext_) ext_->allreduce_max_host(tv, 5);
+        t.total_ms = tv[0], t.loop_ms = tv[1], t.exchange_ms = tv[2], t.comm_ms = tv[3];
+        t.error_ms = tv[4];
+        res.t = t;
+        res.solve_ms.push_back(t.total_ms);
+        return res;
+    }
+
+private:
+    // ---- setup ------------------------------------------------------------------------
+    void setup() {
+        const int A = int(128 / sizeof(T));  // alignment in elements
+        auto tabx = prob_.table_x(), taby = prob_.table_y(), tabz = prob_.table_z();
+        ct_ = prob_.table_t();
+        HIP_CHECK(hipStreamCreateWithFlags(&s_comp_, hipStreamNonBlocking));
+        HIP_CHECK(hipStreamCreateWithFlags(&s_comm_, hipStreamNonBlocking));
+        HIP_CHECK(hipEventCreateWithFlags(&ev_start_, hipEventDefault));
+        HIP_CHECK(hipEventCreateWithFlags(&ev_end_, hipEventDefault));
+        HIP_CHECK(hipEventCreateWithFlags(&ev_layer_, hipEventDisableTiming));
+        HIP_CHECK(hipEventCreateWithFlags(&ev_halo_, hipEventDisableTiming));
+        ranks_.resize(local_.size());
+        const bool have_dims = cfg_.dims[0] || cfg_.dims[1] || cfg_.dims[2];
+        for (size_t q = 0; q < local_.size(); ++q) {
+            auto& R = ranks_[q];
+            R.topo = Topology::make(prob_.N, world_, local_[q], have_dims ? cfg_.dims : nullptr);
+            const int X = R.topo.X(), Y = R.topo.Y(), Z = R.topo.Z();
+            R.gv.nx = X + 2;
+            R.gv.ny = Y + 2;
+            R.gv.nz = Z + 2;
+            R.gv.sj = ((Z + 2 + A - 1) / A) * A;
+            R.gv.si = i64(R.gv.ny) * R.gv.sj;
+            R.lead = A - 1;
+            const size_t elems = size_t(R.lead) + size_t(R.gv.nx) * size_t(R.gv.si);
+            for (int l = 0; l < 3; ++l) {
+                HIP_CHECK(hipMalloc(&R.alloc[l], elems * sizeof(T)));
+                R.g[l] = R.alloc[l] + R.lead;
+            }
+            auto upload = [&](const std::vector<double>& tab, int n, int off) {
+                std::vector<T> v(n + 2, T(0));
+                for (int i = 1; i <= n; ++i) v[i] = T(tab[off + i - 1]);
+                T* d = nullptr;
+                HIP_CHECK(hipMalloc(&d, v.size() * sizeof(T)));
+                HIP_CHECK(hipMemcpy(d, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice));
+                return d;
+            };
+            R.tx = upload(tabx, X, R.topo.off[0]);
+            R.ty = upload(taby, Y, R.topo.off[1]);
+            R.tz = upload(tabz, Z, R.topo.off[2]);
+            R.plan = make_halo_plan(R.topo, R.gv.si, R.gv.nz);
+            if (R.plan.self_x) W3D_REQUIRE(X >= 3, "periodic self-wrap needs >= 3 x planes");
+            R.sbuf.assign(R.plan.sends.size(), nullptr);
+            R.rbuf.assign(R.plan.recvs.size(), nullptr);
+            for (size_t m = 0; m < R.plan.sends.size(); ++m)
+                if (R.plan.sends[m].axis != 0)
+                    HIP_CHECK(hipMalloc(&R.sbuf[m], R.plan.sends[m].count * sizeof(T)));
+            for (size_t m = 0; m < R.plan.recvs.size(); ++m)
+                if (R.plan.recvs[m].axis != 0)
+                    HIP_CHECK(hipMalloc(&R.rbuf[m], R.plan.recvs[m].count * sizeof(T)));
+            HIP_CHECK(hipMalloc(&R.err, sizeof(u64) * (prob_.K + 1) * kSlotsPerLayer));
+
+            R.compute = R.topo.compute_box();
+            R.error = R.topo.error_box();
+            R.owned = R.topo.owned_box();
+            const auto& t = R.topo;
+            R.zero_mask = (t.nbr[2][0] < 0 ? 1 : 0) | (t.nbr[2][1] < 0 ? 2 : 0) |
+                          (t.nbr[1][0] < 0 ? 4 : 0) | (t.nbr[1][1] < 0 ? 8 : 0);
+            if (R.plan.self_x) {
+                R.wrap.src[0] = t.x_send_plus();   // global N-1 -> ghost 0
+                R.wrap.dst[0] = 0;
+                R.wrap.src[1] = t.x_send_minus();  // global 1   -> ghost X+1
+                R.wrap.dst[1] = X + 1;
+            }
+            for (size_t m = 0; m < R.plan.sends.size(); ++m) {
+                const auto& f = R.plan.sends[m];
+                if (f.axis == 1) {
+                    R.pack.ybuf[f.side] = R.sbuf[m];
+                    R.pack.yj[f.side] = f.side ? Y : 1;
+                } else if (f.axis == 2) {
+                    R.pack.zbuf[f.side] = R.sbuf[m];
+                    R.pack.zk[f.side] = f.side ? Z : 1;
+                }
+            }
+            // interior = compute box minus the layer next to every remote ghost
+            Box c = R.compute, in = c;
+            if (!R.plan.self_x) in.i0 = std::max(in.i0, 2), in.i1 = std::min(in.i1, X - 1);
+            if (t.nbr[1][0] >= 0) in.j0 = std::max(in.j0, 2);
+            if (t.nbr[1][1] >= 0) in.j1 = std::min(in.j1, Y - 1);
+            if (t.nbr[2][0] >= 0) in.k0 = std::max(in.k0, 2);
+            if (t.nbr[2][1] >= 0) in.k1 = std::min(in.k1, Z - 1);
+            R.interior = in;
+            R.shell.clear();
+            auto add = [&](Box b) {
+                if (!b.empty()) R.shell.push_back(b);
+            };
+            if (in.empty()) {
+                add(c);
+            } else {
+                add({c.i0, in.i0 - 1, c.j0, c.j1, c.k0, c.k1});
+                add({in.i1 + 1, c.i1, c.j0, c.j1, c.k0, c.k1});
+                add({in.i0, in.i1, c.j0, in.j0 - 1, c.k0, c.k1});
+                add({in.i0, in.i1, in.j1 + 1, c.j1, c.k0, c.k1});
+                add({in.i0, in.i1, in.j0, in.j1, c.k0, in.k0 - 1});
+                add({in.i0, in.i1, in.j0, in.j1, in.k1 + 1, c.k1});
+            }
+        }
+        host_err_.assign(size_t(prob_.K + 1) * kSlotsPerLayer, 0);
+    }
+
+    void release() {
+        for (auto& R : ranks_) {
+            for (int l = 0; l < 3; ++l) (void)hipFree(R.alloc[l]);
+            (void)hipFree(R.tx);
+            (void)hipFree(R.ty);
+            (void)hipFree(R.tz);
+            for (auto* p : R.sbuf) (void)hipFree(p);
+            for (auto* p : R.rbuf) (void)hipFree(p);
+            (void)hipFree(R.err);
+        }
+        ranks_.clear();
+        if (s_comp_) (void)hipStreamDestroy(s_comp_);
+        if (s_comm_) (void)hipStreamDestroy(s_comm_);
+        for (auto e : {ev_start_, ev_end_, ev_layer_, ev_halo_})
+            if (e) (void)hipEventDestroy(e);
+        for (auto e : prof_) (void)hipEventDestroy(e);
+        s_comp_ = s_comm_ = nullptr;
+    }
+
+    // ---- helpers ----------------------------------------------------------------------
+    T* plane(DevRank<T>& R, int level, int i) { return R.g[level] + i64(i) * R.gv.si; }
+
+    int send_plane(const DevRank<T>& R, int side) const {
+        return side ? R.topo.x_send_plus() : R.topo.x_send_minus();
+    }
+
+    void* send_ptr(DevRank<T>& R, size_t m, int n) {
+        const auto& f = R.plan.sends[m];
+        if (f.axis == 0) return plane(R, n % 3, send_plane(R, f.side));
+        return R.sbuf[m];
+    }
+    void* recv_ptr(DevRank<T>& R, size_t m, int n) {
+        const auto& f = R.plan.recvs[m];
+        if (f.axis == 0) return plane(R, n % 3, f.side ? R.topo.X() + 1 : 0);
+        return R.rbuf[m];
+    }
+
+    StepCoefs coefs(int n) const {
+        StepCoefs c;
+        c.hx2 = prob_.hx2;
+        c.hy2 = prob_.hy2;
+        c.hz2 = prob_.hz2;
+        c.coef = n == 1 ? prob_.coef_first : prob_.coef;
+        c.ct = ct_[n];
+        return c;
+    }
+
+    void step_boxes(DevRank<T>& R, int n, const Box* boxes, int nbox, StepKernel kind,
+                    hipStream_t s) {
+        const T* u1 = R.g[(n + 2) % 3];
+        const T* u2 = R.g[(n + 1) % 3];
+        launch_step<T>(kind, n == 1, u1, u2, R.g[n % 3], R.gv, boxes, nbox, R.error.i0,
+                       R.error.i1, R.wrap, R.pack, R.tx, R.ty, R.tz, coefs(n),
+                       R.err + size_t(n) * kSlotsPerLayer, cfg_.chunk, s);
+    }
+
+    void pack_faces(DevRank<T>& R, int n, hipStream_t s, bool to_buf) {
+        FaceOp<T> ops[4];
+        int k = 0;
+        const auto& list = to_buf ? R.plan.sends : R.plan.recvs;
+        for (size_t m = 0; m < list.size(); ++m) {
+            const auto& f = list[m];
+            if (f.axis == 0) continue;
+            FaceOp<T>& o = ops[k++];
+            o.buf = to_buf ? R.sbuf[m] : R.rbuf[m];
+            o.axis = f.axis;
+            if (to_buf) o.index = f.side ? R.topo.ext[f.axis] : 1;
+            else o.index = f.side ? R.topo.ext[f.axis] + 1 : 0;
+        }
+        launch_faces<T>(R.g[n % 3], R.gv, ops, k, to_buf, s);
+    }
+
+    void inject_after_exchange(DevRank<T>& R, int n, hipStream_t s) {
+        if (fault_.kind == "drop_face" && fault_.hits(R.topo.rank, n))
+            HIP_CHECK(hipMemsetAsync(plane(R, n % 3, 0), 0, R.gv.si * sizeof(T), s));
+    }
+    void inject_after_compute(DevRank<T>& R, int n, hipStream_t s) {
+        if (fault_.kind == "nan" && fault_.hits(R.topo.rank, n)) {
+            const Box& b = R.compute;
+            if (b.empty()) return;
+            T* p = R.g[n % 3] + i64((b.i0 + b.i1) / 2) * R.gv.si + i64((b.j0 + b.j1) / 2) * R.gv.sj +
+                   (b.k0 + b.k1) / 2;
+            HIP_CHECK(hipMemsetAsync(p, 0xFF, sizeof(T), s));
+        }
+    }
+
+    // Exchange of layer n, issued on stream s (loopback: all ranks; transport: this rank).
+    void exchange(int n, hipStream_t s) {
+        if (ext_) {
+            auto& R = ranks_[0];
+            std::vector<Message> snd, rcv;
+            for (size_t m = 0; m < R.plan.sends.size(); ++m)
+                snd.push_back({R.plan.sends[m].peer, R.plan.sends[m].tag, send_ptr(R, m, n),
+                               size_t(R.plan.sends[m].count) * sizeof(T)});
+            for (size_t m = 0; m < R.plan.recvs.size(); ++m)
+                rcv.push_back({R.plan.recvs[m].peer, R.plan.recvs[m].tag, recv_ptr(R, m, n),
+                               size_t(R.plan.recvs[m].count) * sizeof(T)});
+            if (!snd.empty() || !rcv.empty()) ext_->exchange(snd, rcv, s);
+            pack_faces(R, n, s, false);
+            inject_after_exchange(R, n, s);
+            return;
+        }
+        for (auto& S : ranks_)
+            for (size_t m = 0; m < S.plan.sends.size(); ++m) {
+                const auto& f = S.plan.sends[m];
+                auto& D = ranks_[f.peer];
+                bool done = false;
+                for (size_t q = 0; q < D.plan.recvs.size(); ++q) {
+                    const auto& g = D.plan.recvs[q];
+                    if (g.peer == S.topo.rank && g.tag == f.tag) {
+                        W3D_REQUIRE(g.count == f.count, "halo size mismatch");
+                        HIP_CHECK(hipMemcpyAsync(recv_ptr(D, q, n), send_ptr(S, m, n),
+                                                 f.count * sizeof(T), hipMemcpyDeviceToDevice, s));
+                        done = true;
+                        break;
+                    }
+                }
+                W3D_REQUIRE(done, "unmatched halo message");
+            }
+        for (auto& R : ranks_) {
+            pack_faces(R, n, s, false);
+            inject_after_exchange(R, n, s);
+        }
+    }
+
+    void prof_mark(hipStream_t s, int slot) {
+        if (!cfg_.profile) return;
+        hipEvent_t e;
+        HIP_CHECK(hipEventCreate(&e));
+        HIP_CHECK(hipEventRecord(e, s));
+        prof_.push_back(e);
+        prof_slot_.push_back(slot);
+    }
+
+    // ---- time loop --------------------------------------------------------------------
+    void solve(RunResult& res, Timings& tm) {
+        const int K = prob_.K;
+        for (auto e : prof_) (void)hipEventDestroy(e);
+        prof_.clear();
+        prof_slot_.clear();
+        for (auto& R : ranks_) {
+            for (int l = 0; l < 3; ++l)
+                HIP_CHECK(hipMemsetAsync(R.alloc[l], 0,
+                                         (size_t(R.lead) + size_t(R.gv.nx) * R.gv.si) * sizeof(T),
+                                         s_comp_));
+            launch_init_err(R.err, K + 1, s_comp_);
+        }
+        HIP_CHECK(hipStreamSynchronize(s_comp_));
+        if (ext_) ext_->barrier();
+
+        auto wall0 = clk::now();
+        HIP_CHECK(hipEventRecord(ev_start_, s_comp_));
+        int start = 1;
+        res.resumed_from = -1;
+        if (!cfg_.resume_dir.empty()) {
+            start = load_checkpoints() + 1;
+            res.resumed_from = start - 1;
+        } else {
+            prof_mark(s_comp_, 0);
+            for (auto& R : ranks_) {
+                launch_init<T>(R.g[0], R.gv, R.owned, R.wrap, R.tx, R.ty, R.tz, ct_[0], R.err,
+                               s_comp_);
+                pack_faces(R, 0, s_comp_, true);
+            }
+            prof_mark(s_comp_, 1);
+            if (K >= 1) issue_exchange(0);
+        }
+        res.aborted = false;
+        int done = start - 1;
+        for (int n = start; n <= K; ++n) {
+            prof_mark(s_comp_, 0);
+            for (auto& R : ranks_)
+                if (n <= 3 || n == start) launch_zero_faces<T>(R.g[n % 3], R.gv, R.zero_mask, s_comp_);
+            if (overlap_) {
+                for (auto& R : ranks_)
+                    if (!R.interior.empty()) step_boxes(R, n, &R.interior, 1, kind_, s_comp_);
+                HIP_CHECK(hipStreamWaitEvent(s_comp_, ev_halo_, 0));
+                for (auto& R : ranks_)
+                    if (!R.shell.empty())
+                        step_boxes(R, n, R.shell.data(), int(R.shell.size()), StepKernel::Naive,
+                                   s_comp_);
+            } else {
+                for (auto& R : ranks_) step_boxes(R, n, &R.compute, 1, kind_, s_comp_);
+            }
+            for (auto& R : ranks_) inject_after_compute(R, n, s_comp_);
+            prof_mark(s_comp_, 1);
+            if (n < K) issue_exchange(n);
+            done = n;
+            if (cfg_.checkpoint_every > 0 && n % cfg_.checkpoint_every == 0 && n < K)
+                save_checkpoints(n);
+            if (cfg_.check_every > 0 && (n % cfg_.check_every == 0 || n == K)) {
+                if (check_layer(n, res)) break;
+            }
+        }
+        res.layers_done = done;
+
+        // final max-reduction of the per-layer slots (mpi_new.cpp:358-361)
+        prof_mark(s_comp_, 4);
+        const size_t nslot = size_t(K + 1) * kSlotsPerLayer;
+        std::vector<u64> acc(nslot, 0);
+        if (ext_) {
+            HIP_CHECK(hipStreamWaitEvent(s_comp_, ev_halo_, 0));
+            ext_->allreduce_max_u64(ranks_[0].err, nslot, s_comp_);
+        }
+        for (auto& R : ranks_) {
+            HIP_CHECK(hipMemcpyAsync(host_err_.data(), R.err, nslot * sizeof(u64),
+                                     hipMemcpyDeviceToHost, s_comp_));
+            HIP_CHECK(hipStreamSynchronize(s_comp_));
+            for (size_t q = 0; q < nslot; ++q) acc[q] = std::max(acc[q], host_err_[q]);
+        }
+        prof_mark(s_comp_, 5);
+        HIP_CHECK(hipEventRecord(ev_end_, s_comp_));
+        HIP_CHECK(hipEventSynchronize(ev_end_));
+        float ms = 0;
+        HIP_CHECK(hipEventElapsedTime(&ms, ev_start_, ev_end_));
+        tm.total_ms = ms;
+        (void)wall0;
+        res.max_abs.assign(K + 1, kErrInit);
+        res.max_rel.assign(K + 1, kErrInit);
+        for (int n = 0; n <= K; ++n) {
+            res.max_abs[n] = decode_max_key(acc[size_t(n) * 3 + 0]);
+            res.max_rel[n] = decode_max_key(acc[size_t(n) * 3 + 1]);
+        }
+        if (res.resumed_from >= 0)
+            for (int n = 0; n <= res.resumed_from && n < int(ckpt_abs_.size()); ++n)
+                res.max_abs[n] = ckpt_abs_[n], res.max_rel[n] = ckpt_rel_[n];
+        if (cfg_.profile) collect_profile(tm);
+        else tm.loop_ms = tm.total_ms;
+    }
+
+    // exchange of layer n: overlapped on the comm stream, or inline on the compute stream
+    void issue_exchange(int n) {
+        if (overlap_) {
+            HIP_CHECK(hipEventRecord(ev_layer_, s_comp_));
+            HIP_CHECK(hipStreamWaitEvent(s_comm_, ev_layer_, 0));
+            prof_mark(s_comm_, 2);
+            exchange(n, s_comm_);
+            prof_mark(s_comm_, 3);
+            HIP_CHECK(hipEventRecord(ev_halo_, s_comm_));
+        } else {
+            bool any = false;
+            for (auto& R : ranks_) any |= !R.plan.sends.empty() || fault_.kind == "drop_face";
+            if (!any) return;
+            prof_mark(s_comp_, 2);
+            exchange(n, s_comp_);
+            prof_mark(s_comp_, 3);
+            HIP_CHECK(hipEventRecord(ev_halo_, s_comp_));
+        }
+    }
+
+    void collect_profile(Timings& tm) {
+        HIP_CHECK(hipDeviceSynchronize());
+        double sum[3] = {0, 0, 0};  // loop, exchange, error
+        for (size_t q = 0; q + 1 < prof_.size(); ++q) {
+            const int a = prof_slot_[q];
+            if (a != 0 && a != 2 && a != 4) continue;
+            for (size_t r = q + 1; r < prof_.size(); ++r)
+                if (prof_slot_[r] == a + 1) {
+                    float ms = 0;
+                    HIP_CHECK(hipEventElapsedTime(&ms, prof_[q], prof_[r]));
+                    sum[a / 2] += ms;
+                    break;
+                }
+        }
+        tm.loop_ms = sum[0];
+        tm.exchange_ms = sum[1];
+        tm.comm_ms = sum[1];
+        tm.error_ms = sum[2];
+    }
+
+    bool check_layer(int n, RunResult& res) {
+        HIP_CHECK(hipStreamSynchronize(s_comp_));
+        double v[2] = {kErrInit, 0.0};
+        for (auto& R : ranks_) {
+            u64 h[3];
+            HIP_CHECK(hipMemcpy(h, R.err + size_t(n) * 3, sizeof(h), hipMemcpyDeviceToHost));
+            v[0] = std::max(v[0], decode_max_key(h[0]));
+            v[1] = std::max(v[1], double(h[2]));
+        }
+        if (ext_) ext_->allreduce_max_host(v, 2);
+        if (layer_diverged(v[0], v[1] != 0.0)) {
+            res.aborted = true;
+            res.abort_layer = n;
+            res.abort_reason = v[1] != 0.0 ? "non-finite values" : "error out of range";
+            return true;
+        }
+        return false;
+    }
+
+    // ---- checkpoint / resume ------------------------------------------------------------
+    std::vector<double> global_errors_upto(int n) {
+        const size_t nslot = size_t(prob_.K + 1) * 3;
+        std::vector<u64> h(nslot);
+        std::vector<double> a(prob_.K + 1, kErrInit), r(prob_.K + 1, kErrInit);
+        HIP_CHECK(hipStreamSynchronize(s_comp_));
+        for (auto& R : ranks_) {
+            HIP_CHECK(hipMemcpy(h.data(), R.err, nslot * sizeof(u64), hipMemcpyDeviceToHost));
+            for (int q = 0; q <= n; ++q) {
+                a[q] = std::max(a[q], decode_max_key(h[size_t(q) * 3]));
+                r[q] = std::max(r[q], decode_max_key(h[size_t(q) * 3 + 1]));
+            }
+        }
+        if (ext_) {
+            ext_->allreduce_max_host(a.data(), a.size());
+            ext_->allreduce_max_host(r.data(), r.size());
+        }
+        a.insert(a.end(), r.begin(), r.end());
+        return a;
+    }
+
+    void save_checkpoints(int n) {
+        std::vector<double> ar = global_errors_upto(n);
+        std::vector<double> a(ar.begin(), ar.begin() + prob_.K + 1), r(ar.begin() + prob_.K + 1, ar.end());
+        HIP_CHECK(hipDeviceSynchronize());
+        for (auto& R : ranks_) {
+            const size_t elems = size_t(R.gv.nx) * R.gv.si;
+            std::vector<T> prev(elems), cur(elems);
+            HIP_CHECK(hipMemcpy(prev.data(), R.g[(n + 2) % 3], elems * sizeof(T), hipMemcpyDeviceToHost));
+            HIP_CHECK(hipMemcpy(cur.data(), R.g[n % 3], elems * sizeof(T), hipMemcpyDeviceToHost));
+            CheckpointHeader h = make_header(cfg_, R.topo, n, sizeof(T));
+            write_checkpoint(cfg_.checkpoint_dir, h, prev.data(), cur.data(), R.gv.nx, R.gv.ny,
+                             R.gv.nz, R.gv.sj, a, r);
+        }
+    }
+
+    int load_checkpoints() {
+        int n = -1;
+        HIP_CHECK(hipDeviceSynchronize());
+        for (auto& R : ranks_) {
+            const size_t elems = size_t(R.gv.nx) * R.gv.si;
+            std::vector<T> lv[3] = {std::vector<T>(elems, T(0)), std::vector<T>(elems, T(0)),
+                                    std::vector<T>(elems, T(0))};
+            CheckpointHeader h = make_header(cfg_, R.topo, 0, sizeof(T));
+            int got = read_checkpoint(cfg_.resume_dir, h, lv, R.gv.nx, R.gv.ny, R.gv.nz, R.gv.sj,
+                                      ckpt_abs_, ckpt_rel_);
+            W3D_REQUIRE(n < 0 || got == n, "checkpoint layers differ between ranks");
+            n = got;
+            for (int l = 0; l < 3; ++l)
+                HIP_CHECK(hipMemcpy(R.g[l], lv[l].data(), elems * sizeof(T), hipMemcpyHostToDevice));
+            // self-wrap ghosts of both levels, then face packs for the remote exchange
+            for (int lvl : {n - 1, n}) {
+                if (R.plan.self_x) {
+                    HIP_CHECK(hipMemcpy(plane(R, lvl % 3, 0), plane(R, lvl % 3, R.topo.x_send_plus()),
+                                        R.gv.si * sizeof(T), hipMemcpyDeviceToDevice));
+                    HIP_CHECK(hipMemcpy(plane(R, lvl % 3, R.topo.X() + 1),
+                                        plane(R, lvl % 3, R.topo.x_send_minus()),
+                                        R.gv.si * sizeof(T), hipMemcpyDeviceToDevice));
+                }
+            }
+        }
+        for (int lvl : {n - 1, n}) {
+            for (auto& R : ranks_) pack_faces(R, lvl, s_comp_, true);
+            exchange(lvl, s_comp_);
+        }
+        HIP_CHECK(hipEventRecord(ev_halo_, s_comp_));
+        return n;
+    }
+
+    Config cfg_;
+    Transport* ext_;
+    Problem prob_;
+    FaultSpec fault_;
+    StepKernel kind_ = StepKernel::March;
+    bool overlap_ = false;
+    int world_ = 1;
+    std::vector<int> local_;
+    std::vector<DevRank<T>> ranks_;
+    std::vector<double> ct_;
+    std::vector<u64> host_err_;
+    std::vector<double> ckpt_abs_, ckpt_rel_;
+    hipStream_t s_comp_ = nullptr, s_comm_ = nullptr;
+    hipEvent_t ev_start_ = nullptr, ev_end_ = nullptr, ev_layer_ = nullptr, ev_halo_ = nullptr;
+    std::vector<hipEvent_t> prof_;
+    std::vector<int> prof_slot_;
+    double init_ms_ = 0;
+};
+
+template <class T>
+class HipSession : public Session {
+public:
+    HipSession(const Config& c, Transport* ext) : s_(c, ext) { s_.init(); }
+    RunResult solve() override { return s_.solve_one(); }
+    double init_ms() const override { return s_.init_ms(); }
+
+private:
+    HipSolver<T> s_;
+};
+
+}  // namespace
+
+std::unique_ptr<Session> make_hip_session(const Config& c, Transport* external) {
+    if (c.device >= 0) HIP_CHECK(hipSetDevice(c.device));
+    if (c.dtype == DType::F64) return std::make_unique<HipSession<double>>(c, external);
+    return std::make_unique<HipSession<float>>(c, external);
+}
+
+RunResult run_hip(const Config& c, Transport* external) {
+    auto s = make_hip_session(c, external);
+    return run_session(*s, c);
+}
+
+}  // namespace wave3d

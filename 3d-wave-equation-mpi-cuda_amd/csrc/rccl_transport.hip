@@ -1,0 +1,162 @@
+#include "rccl_transport.hpp"
+
+#include <arpa/inet.h>
+#include <hip/hip_runtime.h>
+#include <netdb.h>
+#include <netinet/in.h>
+#include <rccl/rccl.h>
+#include <sys/socket.h>
+#include <unistd.h>
+
+#include <chrono>
+#include <cstring>
+#include <thread>
+#include <vector>
+
+namespace wave3d {
+
+#define NCCL_CHECK(x)                                                                     \
+    do {                                                                                  \
+        ncclResult_t r_ = (x);                                                            \
+        if (r_ != ncclSuccess)                                                            \
+            throw ::wave3d::Error(std::string("RCCL error ") + ncclGetErrorString(r_) +  \
+                                  " at " __FILE__ ":" + std::to_string(__LINE__));        \
+    } while (0)
+#define HIP_CHECK_T(x)                                                                 \
+    do {                                                                               \
+        hipError_t e_ = (x);                                                           \
+        if (e_ != hipSuccess)                                                          \
+            throw ::wave3d::Error(std::string("HIP error ") + hipGetErrorString(e_) + \
+                                  " at " __FILE__ ":" + std::to_string(__LINE__));     \
+    } while (0)
+
+static_assert(sizeof(ncclUniqueId) == kRcclIdBytes, "unexpected ncclUniqueId size");
+
+std::string rccl_unique_id() {
+    ncclUniqueId id;
+    NCCL_CHECK(ncclGetUniqueId(&id));
+    return std::string(reinterpret_cast<const char*>(&id), sizeof(id));
+}
+
+struct RcclTransport::Impl {
+    ncclComm_t comm = nullptr;
+    hipStream_t side = nullptr;   // for host-value collectives
+    double* scratch = nullptr;    // device scratch for allreduce_max_host
+    size_t scratch_n = 0;
+};
+
+RcclTransport::RcclTransport(int rank, int size, const std::string& uid, int device)
+    : impl_(new Impl), rank_(rank), size_(size) {
+    W3D_REQUIRE(uid.size() == sizeof(ncclUniqueId), "bad RCCL unique id");
+    HIP_CHECK_T(hipSetDevice(device));
+    ncclUniqueId id;
+    std::memcpy(&id, uid.data(), sizeof(id));
+    NCCL_CHECK(ncclCommInitRank(&impl_->comm, size, id, rank));
+    HIP_CHECK_T(hipStreamCreateWithFlags(&impl_->side, hipStreamNonBlocking));
+}
+
+RcclTransport::~RcclTransport() {
+    if (impl_->scratch) (void)hipFree(impl_->scratch);
+    if (impl_->side) (void)hipStreamDestroy(impl_->side);
+    if (impl_->comm) (void)ncclCommDestroy(impl_->comm);
+}
+
+void RcclTransport::exchange(const std::vector<Message>& sends, const std::vector<Message>& recvs,
+                             void* stream) {
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    NCCL_CHECK(ncclGroupStart());
+    for (const auto& m : sends)
+        NCCL_CHECK(ncclSend(m.ptr, m.bytes, ncclChar, m.peer, impl_->comm, s));
+    for (const auto& m : recvs)
+        NCCL_CHECK(ncclRecv(m.ptr, m.bytes, ncclChar, m.peer, impl_->comm, s));
+    NCCL_CHECK(ncclGroupEnd());
+}
+
+void RcclTransport::allreduce_max_u64(u64* data, size_t n, void* stream) {
+    NCCL_CHECK(ncclAllReduce(data, data, n, ncclUint64, ncclMax, impl_->comm,
+                             static_cast<hipStream_t>(stream)));
+}
+
+void RcclTransport::allreduce_max_host(double* data, size_t n) {
+    if (impl_->scratch_n < n) {
+        if (impl_->scratch) HIP_CHECK_T(hipFree(impl_->scratch));
+        HIP_CHECK_T(hipMalloc(&impl_->scratch, n * sizeof(double)));
+        impl_->scratch_n = n;
+    }
+    HIP_CHECK_T(hipMemcpyAsync(impl_->scratch, data, n * sizeof(double), hipMemcpyHostToDevice,
+                               impl_->side));
+    NCCL_CHECK(ncclAllReduce(impl_->scratch, impl_->scratch, n, ncclFloat64, ncclMax, impl_->comm,
+                             impl_->side));
+    HIP_CHECK_T(hipMemcpyAsync(data, impl_->scratch, n * sizeof(double), hipMemcpyDeviceToHost,
+                               impl_->side));
+    HIP_CHECK_T(hipStreamSynchronize(impl_->side));
+    check_async();
+}
+
+void RcclTransport::barrier() {
+    double v = 0;
+    allreduce_max_host(&v, 1);
+}
+
+void RcclTransport::check_async() const {
+    ncclResult_t st = ncclSuccess;
+    NCCL_CHECK(ncclCommGetAsyncError(impl_->comm, &st));
+    if (st != ncclSuccess) throw Error(std::string("RCCL async error: ") + ncclGetErrorString(st));
+}
+
+// ---- TCP rendezvous -------------------------------------------------------------------
+std::string tcp_share_unique_id(int rank, int size, const std::string& addr, int port) {
+    if (size == 1) return rccl_unique_id();
+    if (rank == 0) {
+        std::string id = rccl_unique_id();
+        int fd = socket(AF_INET, SOCK_STREAM, 0);
+        W3D_REQUIRE(fd >= 0, "socket() failed");
+        int one = 1;
+        setsockopt(fd, SOL_SOCKET, SO_REUSEADDR, &one, sizeof(one));
+        sockaddr_in a{};
+        a.sin_family = AF_INET;
+        a.sin_port = htons(uint16_t(port));
+        a.sin_addr.s_addr = htonl(INADDR_ANY);
+        W3D_REQUIRE(bind(fd, (sockaddr*)&a, sizeof(a)) == 0, "bind() failed on port " + std::to_string(port));
+        W3D_REQUIRE(listen(fd, size) == 0, "listen() failed");
+        for (int q = 1; q < size; ++q) {
+            int c = accept(fd, nullptr, nullptr);
+            W3D_REQUIRE(c >= 0, "accept() failed");
+            size_t off = 0;
+            while (off < id.size()) {
+                ssize_t w = send(c, id.data() + off, id.size() - off, 0);
+                W3D_REQUIRE(w > 0, "send() failed");
+                off += size_t(w);
+            }
+            close(c);
+        }
+        close(fd);
+        return id;
+    }
+    std::string id(kRcclIdBytes, '\0');
+    addrinfo hints{}, *res = nullptr;
+    hints.ai_family = AF_INET;
+    hints.ai_socktype = SOCK_STREAM;
+    W3D_REQUIRE(getaddrinfo(addr.c_str(), std::to_string(port).c_str(), &hints, &res) == 0,
+                "cannot resolve " + addr);
+    int fd = -1;
+    for (int attempt = 0; attempt < 600; ++attempt) {  // up to ~60 s for rank 0 to listen
+        fd = socket(AF_INET, SOCK_STREAM, 0);
+        if (connect(fd, res->ai_addr, res->ai_addrlen) == 0) break;
+        close(fd);
+        fd = -1;
+        std::this_thread::sleep_for(std::chrono::milliseconds(100));
+    }
+    freeaddrinfo(res);
+    W3D_REQUIRE(fd >= 0, "cannot connect to rank 0 at " + addr + ":" + std::to_string(port));
+    size_t off = 0;
+    while (off < id.size()) {
+        ssize_t r = recv(fd, &id[off], id.size() - off, 0);
+        W3D_REQUIRE(r > 0, "recv() failed");
+        off += size_t(r);
+    }
+    close(fd);
+    return id;
+}
+
+}  // namespace wave3d

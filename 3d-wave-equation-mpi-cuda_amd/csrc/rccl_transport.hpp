@@ -1,0 +1,47 @@
+// RCCL point-to-point halo transport over xGMI.
+//
+// Replaces the reference's host-staged blocking MPI_Sendrecv chain (cuda_sol.cpp:230-312):
+// every face of one exchange is posted inside one ncclGroupStart/End on the caller's
+// stream, straight from device memory — no pinned staging, no host sync. The final error
+// reduction is one ncclAllReduce(ncclMax) on the order-preserving u64 keys.
+#pragma once
+
+#include <memory>
+#include <string>
+
+#include "halo.hpp"
+
+namespace wave3d {
+
+constexpr int kRcclIdBytes = 128;  // sizeof(ncclUniqueId)
+
+std::string rccl_unique_id();  // 128 raw bytes
+
+class RcclTransport : public Transport {
+public:
+    // Must be called with `device` as the current device on this thread.
+    RcclTransport(int rank, int size, const std::string& unique_id, int device);
+    ~RcclTransport() override;
+    std::string name() const override { return "rccl"; }
+    int rank() const override { return rank_; }
+    int size() const override { return size_; }
+    bool device() const override { return true; }
+    void exchange(const std::vector<Message>& sends, const std::vector<Message>& recvs,
+                  void* stream) override;
+    void allreduce_max_u64(u64* data, size_t n, void* stream) override;
+    void allreduce_max_host(double* data, size_t n) override;
+    void barrier() override;
+    // Async-error watchdog: throws if the communicator reported an error.
+    void check_async() const;
+
+private:
+    struct Impl;
+    std::unique_ptr<Impl> impl_;
+    int rank_, size_;
+};
+
+// Minimal TCP rendezvous for the standalone program (torchrun-style env: RANK, WORLD_SIZE,
+// MASTER_ADDR, MASTER_PORT): rank 0 generates the RCCL id and serves it to the others.
+std::string tcp_share_unique_id(int rank, int size, const std::string& addr, int port);
+
+}  // namespace wave3d

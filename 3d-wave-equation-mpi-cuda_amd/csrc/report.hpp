@@ -1,0 +1,55 @@
+// Results, the reference-format output file and a JSON summary.
+#pragma once
+
+#include <string>
+#include <vector>
+
+#include "config.hpp"
+#include "problem.hpp"
+#include "topology.hpp"
+
+namespace wave3d {
+
+struct Timings {
+    double init_ms = 0;      // allocation + table upload ("grids initialized in")
+    double total_ms = 0;     // IC through last layer ("numerical solution calculated in")
+    double loop_ms = 0;      // stencil / IC / boundary kernels
+    double exchange_ms = 0;  // pack + transport + unpack (host-device exchange in cuda_sol)
+    double comm_ms = 0;      // transport only ("total MPI exchange time")
+    double error_ms = 0;     // error reduction finalisation
+};
+
+struct RunResult {
+    int N = 0, K = 0, nprocs = 1, Np = 1;
+    int dims[3] = {1, 1, 1};
+    DType dtype = DType::F64;
+    std::string backend;     // "hip" | "cpu"
+    std::string kernel;      // stencil variant actually used
+    std::string transport;   // "self" | "loopback" | "rccl" | "external"
+    double courant = 0;
+    std::vector<double> max_abs, max_rel;  // per layer, max over all ranks
+    Timings t;                             // last timed solve, max over ranks
+    std::vector<double> solve_ms;          // every timed solve (max over ranks)
+    int layers_done = 0;
+    bool aborted = false;
+    int abort_layer = -1;
+    std::string abort_reason;
+    int resumed_from = -1;
+
+    double points() const { return double(N + 1) * double(N + 1) * double(N + 1); }
+    // Mpoints/s = (N+1)^3 * timesteps / t  (BASELINE.md metric definition)
+    double mpts_per_s() const;
+    double mpts_per_s_best() const;
+    double linf_final() const { return max_abs.empty() ? 0.0 : max_abs.back(); }
+};
+
+// Default ostream formatting, identical to the reference's `out << double`.
+std::string fmt_double(double v);
+
+std::string output_filename(const Config& c, const RunResult& r);
+// Text of the output file for the selected flavour (Appendix A).
+std::string format_report(const Config& c, const RunResult& r);
+void write_report(const Config& c, const RunResult& r);  // no-op for ReportFormat::None
+std::string json_summary(const Config& c, const RunResult& r);
+
+}  // namespace wave3d

@@ -1,0 +1,87 @@
+// Point-update arithmetic shared by the OpenMP oracle and the HIP kernels.
+//
+// The operation order is the reference's, term for term, so that with FP contraction off
+// both backends reproduce the reference output bit for bit:
+//   laplace  = 0 + (u[i-1] - 2u + u[i+1])/(hx*hx) + (..y..)/(hy*hy) + (..z..)/(hz*hz)
+//                                                             (mpi_new.cpp:104-111)
+//   layer 1  = u0 + (a2*tau*tau*0.5) * laplace                (mpi_new.cpp:303)
+//   layer n  = (2*u1 - u2) + (a2*tau*tau) * laplace            (mpi_new.cpp:338)
+//   f        = sin(..x..)*sin(..y..)*sin(..z..)*cos(..t..)    (mpi_new.cpp:151)
+//   abs      = |u - f|, rel = |u - f| / |f|                   (mpi_new.cpp:341-342)
+//   max      : if (e > m) m = e   (NaN never wins)            (mpi_new.cpp:343-344)
+#pragma once
+
+#include <cmath>
+
+#ifdef __HIPCC__
+#define W3D_HD __host__ __device__ __forceinline__
+#else
+#define W3D_HD inline
+#endif
+
+namespace wave3d {
+
+template <class T>
+W3D_HD T laplace7(T c, T xm, T xp, T ym, T yp, T zm, T zp, T hx2, T hy2, T hz2) {
+#ifdef __clang__
+#pragma clang fp contract(off)
+#endif
+    T two_c = T(2) * c;
+    T ans = T(0);
+    ans += (xm - two_c + xp) / hx2;
+    ans += (ym - two_c + yp) / hy2;
+    ans += (zm - two_c + zp) / hz2;
+    return ans;
+}
+
+template <class T>
+W3D_HD T leapfrog(T c, T u2, T lap, T coef) {
+#ifdef __clang__
+#pragma clang fp contract(off)
+#endif
+    return (T(2) * c - u2) + coef * lap;
+}
+
+template <class T>
+W3D_HD T taylor_first(T c, T lap, T coef_first) {
+#ifdef __clang__
+#pragma clang fp contract(off)
+#endif
+    return c + coef_first * lap;
+}
+
+template <class T>
+W3D_HD T analytic(T sx, T sy, T sz, T ct) {
+#ifdef __clang__
+#pragma clang fp contract(off)
+#endif
+    return ((sx * sy) * sz) * ct;
+}
+
+W3D_HD double absval(double x) { return __builtin_fabs(x); }
+W3D_HD float absval(float x) { return __builtin_fabsf(x); }
+
+// Updates the running maxima with the reference's NaN-ignoring comparison.
+template <class T>
+W3D_HD void accumulate_error(T u, T f, T& mabs, T& mrel) {
+#ifdef __clang__
+#pragma clang fp contract(off)
+#endif
+    T d = u - f;
+    T ea = absval(d);
+    T er = ea / absval(f);
+    if (ea > mabs) mabs = ea;
+    if (er > mrel) mrel = er;
+}
+
+// True for NaN and +-Inf (x - x is NaN exactly for those).
+template <class T>
+W3D_HD bool nonfinite(T x) {
+#ifdef __clang__
+#pragma clang fp contract(off)
+#endif
+    T z = x - x;
+    return z != z;
+}
+
+}  // namespace wave3d

@@ -1,0 +1,46 @@
+"""Benchmark/validation configurations (BASELINE.json "configs").
+
+The reference defaults (T=1, K=20) are unstable for N >= 256 with L = pi (C > 1/sqrt(3),
+SURVEY §4.2.3), so every GPU config uses a stable K.
+"""
+from __future__ import annotations
+
+from .wave import WaveProblem
+
+# Reference numbers measured on the survey host, Mpoints/s.
+BASELINE_MPTS = {512: 138.5, 1024: 159.8, 128: 96.7}
+# Accuracy goldens: final-layer L-inf abs for L=pi, T=1.
+GOLDEN_LINF = {
+    (32, 20): 1.75963e-04,
+    (64, 20): 4.22698e-05,
+    (128, 20): 8.81051e-06,
+    (256, 40): 2.20262e-06,
+    (512, 100): 6.03381e-07,
+    (1024, 100): 8.04265e-08,
+}
+
+CONFIGS = {
+    # N=128^3 fp64 single-process OpenMP (openmp_sol path, plumbing)
+    "cpu128": dict(problem=WaveProblem(128, timesteps=20), backend="cpu", Np=8),
+    # N=512^3 fp64 on one MI355X
+    "gpu512": dict(problem=WaveProblem(512, timesteps=100), backend="hip", Np=1),
+    # N=512^3 fp64 on 2 MI355X, slab decomposition (2x1x1)
+    "gpu512x2": dict(problem=WaveProblem(512, timesteps=100), backend="hip", Np=2),
+    # N=1024^3 fp64 on 8 MI355X, 2x2x2 blocks
+    "gpu1024x8": dict(problem=WaveProblem(1024, timesteps=100), backend="hip", Np=8),
+    # N=2048^3 fp32 on 8 MI355X
+    "gpu2048x8_fp32": dict(problem=WaveProblem(2048, timesteps=200, dtype="fp32"), backend="hip", Np=8),
+}
+
+
+def weak_scaling_N(n_gpus: int, base_N: int = 512) -> int:
+    """Global N keeping (N+1)^3 / n_gpus ~= (base_N+1)^3 (per-GPU work fixed)."""
+    if n_gpus <= 1:
+        return base_N
+    if n_gpus == 8 and base_N == 512:
+        return 1024  # the BASELINE 8-GPU config (1025^3 / 8 = 134.6M vs 513^3 = 135.0M)
+    return round((base_N + 1) * n_gpus ** (1.0 / 3.0)) - 1
+
+
+def bench_problem(n_gpus: int, timesteps: int = 100, dtype: str = "fp64") -> WaveProblem:
+    return WaveProblem(weak_scaling_N(n_gpus), timesteps=timesteps, dtype=dtype)

@@ -1,0 +1,151 @@
+"""Tensor-level access to the hand-written HIP kernels (for numerics tests and tools).
+
+Tensors are dense ``[nx][ny][nz]`` (k contiguous, one ghost layer) on the current HIP
+device; they are passed to the native kernels as raw pointers on torch's current stream.
+Shapes are validated here *before* any launch (the kernels index with the boxes given).
+The solver itself uses an aligned, padded layout (``csrc/hip_kernels.hpp``); these entry
+points use pitch = nz, which the kernels accept as well.
+"""
+from __future__ import annotations
+
+import torch
+
+from .._native import load
+
+_U64 = (1 << 64) - 1
+
+
+def _C():
+    return load()
+
+
+def _stream() -> int:
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _sfx(t: torch.Tensor) -> str:
+    if t.dtype == torch.float64:
+        return "f64"
+    if t.dtype == torch.float32:
+        return "f32"
+    raise TypeError(f"unsupported dtype {t.dtype}")
+
+
+def _check_grid(*ts: torch.Tensor) -> list[int]:
+    u = ts[0]
+    for t in ts:
+        if not t.is_cuda:
+            raise ValueError("wave3d kernels need HIP device tensors")
+        if t.dim() != 3 or not t.is_contiguous():
+            raise ValueError("grids must be contiguous 3-D [nx][ny][nz] tensors")
+        if t.shape != u.shape or t.dtype != u.dtype:
+            raise ValueError("grid shapes/dtypes differ")
+    nx, ny, nz = u.shape
+    if min(nx, ny, nz) < 3:
+        raise ValueError("grid needs at least one owned node plus ghosts per axis")
+    return [nx, ny, nz, nz, ny * nz]
+
+
+def _check_box(box, gv) -> list[int]:
+    i0, i1, j0, j1, k0, k1 = (int(v) for v in box)
+    nx, ny, nz = gv[0], gv[1], gv[2]
+    if not (1 <= i0 and i1 <= nx - 2 and 1 <= j0 and j1 <= ny - 2 and 1 <= k0 and k1 <= nz - 2):
+        raise ValueError(f"box {box} outside the owned region of a {nx}x{ny}x{nz} grid")
+    return [i0, i1, j0, j1, k0, k1]
+
+
+def _check_tables(u, tx, ty, tz):
+    nx, ny, nz = u.shape
+    for t, n, name in ((tx, nx, "tx"), (ty, ny, "ty"), (tz, nz, "tz")):
+        if not t.is_cuda or t.dtype != u.dtype or t.numel() < n or not t.is_contiguous():
+            raise ValueError(f"table {name} must be a contiguous {u.dtype} device tensor of >= {n}")
+
+
+def new_err(layers: int = 1, device=None) -> torch.Tensor:
+    """Per-layer error slots (abs key, rel key, non-finite flag), initialised on device."""
+    e = torch.empty(layers * 3, dtype=torch.int64, device=device or "cuda")
+    _C().k_init_err(e.data_ptr(), layers, _stream())
+    return e
+
+
+def decode_err(err: torch.Tensor) -> list[tuple[float, float, bool]]:
+    C = _C()
+    v = [int(x) & _U64 for x in err.cpu().tolist()]
+    return [(C.decode_max_key(v[q]), C.decode_max_key(v[q + 1]), v[q + 2] != 0)
+            for q in range(0, len(v), 3)]
+
+
+def step(u1, u2, u, boxes, *, first: bool, err_i, tx, ty, tz, coefs, err,
+         kernel: str = "march", wrap=None, chunk: int = 0, pack=None) -> None:
+    """One leapfrog layer over ``boxes`` (list of (i0,i1,j0,j1,k0,k1), local indices).
+
+    coefs = (hx2, hy2, hz2, coef, ct); err_i = (ei0, ei1) rows entering the error;
+    wrap = (src0, dst0, src1, dst1) periodic self-wrap planes; pack = ([zbuf0, zbuf1,
+    ybuf0, ybuf1] tensors or None, [zk0, zk1, yj0, yj1]).
+    """
+    gv = _check_grid(u1, u2, u)
+    if isinstance(boxes[0], int):
+        boxes = [boxes]
+    if not 1 <= len(boxes) <= 7:
+        raise ValueError("1..7 boxes per launch")
+    bl = [_check_box(b, gv) for b in boxes]
+    _check_tables(u, tx, ty, tz)
+    if err.dtype != torch.int64 or err.numel() < 3 or not err.is_cuda:
+        raise ValueError("err must be >= 3 int64 device slots (new_err())")
+    if wrap is not None:
+        w = [int(v) for v in wrap]
+        for q in range(0, 4, 2):
+            if w[q] >= 0 and not (0 <= w[q + 1] < gv[0] and 1 <= w[q] <= gv[0] - 2):
+                raise ValueError("bad wrap planes")
+    else:
+        w = []
+    pb, pi = [], []
+    if pack is not None:
+        bufs, idx = pack
+        pb = [b.data_ptr() if b is not None else 0 for b in bufs]
+        pi = [int(v) for v in idx]
+        nx, ny, nz = u.shape
+        for q, b in enumerate(bufs):
+            if b is None:
+                continue
+            need = (nx - 2) * (ny if q < 2 else nz)
+            if b.numel() < need or b.dtype != u.dtype:
+                raise ValueError("pack buffer too small")
+    fn = getattr(_C(), "k_step_" + _sfx(u))
+    fn(kernel, bool(first), u1.data_ptr(), u2.data_ptr(), u.data_ptr(), gv, bl, int(err_i[0]),
+       int(err_i[1]), w, tx.data_ptr(), ty.data_ptr(), tz.data_ptr(), [float(c) for c in coefs],
+       err.data_ptr(), int(chunk), _stream(), pb, pi)
+
+
+def init(u, box, *, tx, ty, tz, ct0: float, err, wrap=None) -> None:
+    gv = _check_grid(u)
+    b = _check_box(box, gv)
+    _check_tables(u, tx, ty, tz)
+    getattr(_C(), "k_init_" + _sfx(u))(u.data_ptr(), gv, b, list(wrap or []), tx.data_ptr(),
+                                      ty.data_ptr(), tz.data_ptr(), float(ct0), err.data_ptr(),
+                                      _stream())
+
+
+def zero_faces(u, mask: int) -> None:
+    gv = _check_grid(u)
+    getattr(_C(), "k_zero_faces_" + _sfx(u))(u.data_ptr(), gv, int(mask), _stream())
+
+
+def faces(u, ops, to_buf: bool) -> None:
+    """ops: list of (buffer, axis in {1,2}, plane index). Pack (to_buf) or unpack."""
+    gv = _check_grid(u)
+    nx, ny, nz = u.shape
+    lst = []
+    for buf, axis, index in ops:
+        if axis not in (1, 2):
+            raise ValueError("faces: axis must be 1 (y) or 2 (z)")
+        lim = ny if axis == 1 else nz
+        if not 0 <= index < lim:
+            raise ValueError("faces: plane index out of range")
+        need = (nx - 2) * (nz if axis == 1 else ny)
+        if buf.numel() < need or buf.dtype != u.dtype or not buf.is_cuda:
+            raise ValueError("faces: buffer too small")
+        lst.append((buf.data_ptr(), int(axis), int(index)))
+    if len(lst) > 4:
+        raise ValueError("at most 4 faces per launch")
+    getattr(_C(), "k_faces_" + _sfx(u))(u.data_ptr(), gv, lst, bool(to_buf), _stream())

@@ -1,0 +1,148 @@
+#!/usr/bin/env python3
+"""wave3d benchmark — the reference's headline metric on MI355X.
+
+Metric (BASELINE.json): Mpoints/s (whole node) + L-inf error vs the analytic solution,
+N=512^3 fp64. One benchmark *step* is one complete solve exactly as timed by the reference
+(`numerical solution calculated in`, mpi_new.cpp:325-357): initial condition, Taylor first
+layer, `timesteps` leapfrog layers, the fused per-layer max-error evaluation and the final
+cross-rank MAX reduction. Mpoints/s = (N+1)^3 * timesteps * steps / t_wall.
+
+Scaling is weak: per-GPU work is fixed at ~513^3 nodes, the global grid grows with the GPU
+count (1 GPU: N=512 = BASELINE config 2; 8 GPUs: N=1024 on 2x2x2 = BASELINE config 4).
+Data: the analytic initial condition on a synthetic grid (the reference's own test problem).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+METRIC = "Mpoints/sec (whole node) + L∞ error vs analytic, N=512³ fp64"
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5, help="timed solves")
+    ap.add_argument("--warmup", type=int, default=2, help="untimed solves")
+    ap.add_argument("--N", type=int, default=0, help="override global N (default: weak scaling from 512)")
+    ap.add_argument("--timesteps", type=int, default=100)
+    ap.add_argument("--dtype", default="fp64", choices=["fp64", "fp32"])
+    ap.add_argument("--kernel", default="auto")
+    ap.add_argument("--chunk", type=int, default=0)
+    ap.add_argument("--no-overlap", action="store_true")
+    ap.add_argument("--backend", default="hip", choices=["hip", "cpu"])
+    ap.add_argument("--profile", action="store_true", help="per-phase timers (slower)")
+    a = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    import wave3d
+    from wave3d.models import presets
+    from wave3d.parallel import dist as wdist
+
+    C = wave3d.load_native()
+    rank, world, local = wdist.env_rank()
+    if world != a.gpus and world > 1:
+        print(f"bench: WORLD_SIZE={world} but --gpus {a.gpus}", file=sys.stderr)
+    n_gpus = world if world > 1 else a.gpus
+    if world == 1 and a.gpus > 1:
+        print("bench: --gpus > 1 must be launched with torch.distributed.run (one rank per GPU)",
+              file=sys.stderr)
+        return 2
+
+    transport = None
+    if world > 1:
+        wdist.init_from_env("nccl" if a.backend == "hip" else "gloo")
+        if a.backend == "hip":
+            transport = wdist.rccl_transport(torch.cuda.current_device())
+        else:
+            transport = wdist.TorchHostTransport()
+    elif a.backend == "hip":
+        torch.cuda.set_device(0)
+
+    N = a.N or presets.weak_scaling_N(n_gpus)
+    prob = wave3d.WaveProblem(N, timesteps=a.timesteps, dtype=a.dtype)
+    if not prob.stable():
+        print(f"bench: warning: C={prob.courant:.3f} > 1/sqrt(3) (unstable)", file=sys.stderr)
+    solver = wave3d.WaveSolver(prob, a.backend, transport=transport, Np=n_gpus, kernel=a.kernel,
+                               chunk=a.chunk, overlap=not a.no_overlap, profile=a.profile,
+                               device=(torch.cuda.current_device() if a.backend == "hip" else None))
+    args = solver.args()
+    sess = C.Session(args, a.backend, transport)
+
+    def sync():
+        if a.backend == "hip":
+            torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+
+    res = None
+    for _ in range(a.warmup):
+        res = sess.solve(args)
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        res = sess.solve(args)
+    sync()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64,
+                         device="cuda" if a.backend == "hip" else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    pts = (N + 1) ** 3
+    value = pts * a.timesteps * a.steps / elapsed / 1e6
+    base = presets.BASELINE_MPTS.get(N, presets.BASELINE_MPTS[512])
+    dims = res["dims"]
+    out = {
+        "metric": METRIC,
+        "value": round(value, 3),
+        "unit": "Mpoints/s",
+        "n_gpus": n_gpus,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": round(elapsed / a.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": round(value / base, 3),
+        "dtype": a.dtype,
+        "data": "synthetic (analytic initial condition u=sin(2pi x/Lx)sin(pi y/Ly)sin(pi z/Lz))",
+        "config": {
+            "model": f"wave3d leapfrog 7-point, N={N}^3, L=pi, T=1, timesteps={a.timesteps}",
+            "global_batch": 1,
+            "seq_len": N + 1,
+            "parallelism": f"dd{dims[0]}x{dims[1]}x{dims[2]}" + ("" if n_gpus == 1 else "-rccl"),
+            "N": N,
+            "timesteps": a.timesteps,
+            "kernel": res["kernel"],
+            "overlap": not a.no_overlap,
+        },
+        "linf_abs": res["linf_abs"],
+        "linf_final_layer": res["timesteps"],
+        "courant": round(prob.courant, 4),
+        "solver_ms_per_step": round(sum(res["solve_ms"]) / max(1, len(res["solve_ms"])), 4),
+        "baseline_mpts": base,
+    }
+    if a.profile:
+        out["profile_ms"] = {k: res[k] for k in ("loop_ms", "exchange_ms", "error_ms", "total_ms")}
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    del sess
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,131 @@
+"""End-to-end HIP solver tests on one MI355X: goldens, decomposition invariance (simulated
+ranks, with and without the interior/shell overlap), CPU/GPU bitwise agreement, fp32,
+checkpoint/resume, fault detection, the CLI program."""
+import os
+import subprocess
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _solve(prob, backend="hip", **kw):
+    import wave3d
+
+    return wave3d.WaveSolver(prob, backend, **kw).run()
+
+
+def _fmt(r):
+    from wave3d.utils import fmt6
+
+    return [(fmt6(a), fmt6(b)) for a, b in zip(r.max_abs, r.max_rel)]
+
+
+@pytest.mark.parametrize("kernel", ["march", "naive"])
+def test_golden_n32(C, kernel):
+    import wave3d
+    from wave3d.utils import GOLDEN_N32_K20
+
+    r = _solve(wave3d.WaveProblem(32, timesteps=20), kernel=kernel)
+    assert r.backend == "hip" and r.kernel == kernel
+    assert _fmt(r) == GOLDEN_N32_K20
+
+
+@pytest.mark.parametrize("ranks,overlap", [(2, True), (2, False), (4, True), (8, True), (8, False), (3, True)])
+def test_decomposition_invariance(C, ranks, overlap):
+    import wave3d
+
+    p = wave3d.WaveProblem(40, Lx=1.3, Ly="pi", Lz=2.0, timesteps=15, ic="shifted")
+    base = _solve(p)
+    r = _solve(p, ranks=ranks, overlap=overlap)
+    assert r.transport == "loopback"
+    assert r.max_abs == base.max_abs and r.max_rel == base.max_rel
+
+
+def test_cpu_gpu_bitwise(C):
+    import wave3d
+
+    p = wave3d.WaveProblem(37, Lx=1.7, Ly=2.2, Lz="pi", timesteps=12, ic="shifted")
+    g = _solve(p)
+    c = _solve(p, backend="cpu", threads=4)
+    assert g.max_abs == c.max_abs and g.max_rel == c.max_rel
+
+
+def test_spots_and_shifted(C):
+    import wave3d
+    from wave3d.utils import GOLDEN_SPOTS
+
+    for (N, K, ic), spots in GOLDEN_SPOTS.items():
+        if N > 128:
+            continue
+        got = _fmt(_solve(wave3d.WaveProblem(N, timesteps=K, ic=ic)))
+        for layer, val in spots.items():
+            assert got[layer] == val, (N, K, ic, layer)
+
+
+def test_n512_golden(C):
+    import wave3d
+    from wave3d.utils import GOLDEN_SPOTS
+
+    got = _fmt(_solve(wave3d.WaveProblem(512, timesteps=100)))
+    for layer, val in GOLDEN_SPOTS[(512, 100, "ref")].items():
+        assert got[layer] == val
+
+
+def test_fp32_close(C):
+    import wave3d
+
+    p64 = wave3d.WaveProblem(64, timesteps=20)
+    p32 = wave3d.WaveProblem(64, timesteps=20, dtype="fp32")
+    a, b = _solve(p64), _solve(p32)
+    assert b.max_abs[-1] == pytest.approx(a.max_abs[-1], rel=0.05)
+
+
+def test_checkpoint_resume(C, tmp_path):
+    import wave3d
+
+    p = wave3d.WaveProblem(30, timesteps=12, ic="shifted")
+    full = _solve(p, ranks=2)
+    d = str(tmp_path)
+    _solve(p, ranks=2, checkpoint_every=5, checkpoint_dir=d)
+    assert os.path.exists(os.path.join(d, "ckpt_r0.bin"))
+    res = _solve(p, ranks=2, resume=d)
+    assert res.extra["resumed_from"] == 10
+    assert res.max_abs == full.max_abs and res.max_rel == full.max_rel
+
+
+def test_fault_detection(C):
+    import wave3d
+
+    p = wave3d.WaveProblem(24, timesteps=10)
+    r = _solve(p, check_every=1, fault="nan:0:4")
+    assert r.aborted and r.abort_layer in (4, 5)
+    ok = _solve(p, check_every=1)
+    assert not ok.aborted
+    bad = _solve(p, ranks=2, fault="drop_face:1:3")
+    assert bad.max_abs[-1] > 10 * ok.max_abs[-1]
+
+
+def test_program_cli_matches_cpu(C, gpu_prog, cpu_prog, tmp_path):
+    for prog in (gpu_prog, cpu_prog):
+        subprocess.run([prog, "32", "1", "pi", "pi", "pi", "1", "20", "--format", "new",
+                        "--out-dir", str(tmp_path), "--out-name", os.path.basename(prog) + ".txt"],
+                       check=True, capture_output=True, timeout=120)
+    a = open(tmp_path / "wave3d.txt").read().splitlines()
+    b = open(tmp_path / "wave3d_cpu.txt").read().splitlines()
+    ea = [l for l in a if l.startswith("max abs")]
+    eb = [l for l in b if l.startswith("max abs")]
+    assert ea == eb and len(ea) == 21
+    assert a[0].startswith("grids initialized in") and a[1].startswith("numerical solution calculated in")
+
+
+def test_session_reuse(C):
+    import wave3d
+
+    p = wave3d.WaveProblem(32, timesteps=20)
+    s = wave3d.WaveSolver(p, "hip")
+    args = s.args()
+    sess = C.Session(args, "hip", None)
+    r1 = sess.solve(args)
+    r2 = sess.solve(args)
+    assert r1["max_abs"] == r2["max_abs"]
