@@ -143,7 +143,7 @@ void k_step(const std::string& kind, bool first, uintptr_t u1, uintptr_t u2, uin
     }
     W3D_REQUIRE(coefs.size() == 5, "coefs = (hx2, hy2, hz2, coef, ct)");
     StepCoefs c{coefs[0], coefs[1], coefs[2], coefs[3], coefs[4]};
-    launch_step<T>(kind == "naive" ? StepKernel::Naive : StepKernel::March, first, P<T>(u1),
+    launch_step<T>(parse_kernel_variant(kind), first, P<T>(u1),
                    P<T>(u2), P<T>(u), gview(g), bx.data(), int(bx.size()), ei0, ei1, w, fp,
                    P<T>(tx), P<T>(ty), P<T>(tz), c, P<u64>(err), chunk, (hipStream_t)stream);
 }
@@ -292,6 +292,19 @@ PYBIND11_MODULE(_wave3d_C, m) {
     });
     m.def("k_encode_keys", [](uintptr_t v, uintptr_t k, int n, uintptr_t s) {
         launch_encode_keys(P<double>(v), P<u64>(k), n, (hipStream_t)s);
+    });
+    // raw HIP helpers for Python-side device transports (staged halos in tests/tools)
+    m.def("hip_memcpy", [](uintptr_t dst, uintptr_t src, size_t bytes, uintptr_t stream) {
+        py::gil_scoped_release nogil;
+        hipError_t e = hipMemcpyAsync((void*)dst, (const void*)src, bytes, hipMemcpyDefault,
+                                      (hipStream_t)stream);
+        if (e == hipSuccess) e = hipStreamSynchronize((hipStream_t)stream);
+        if (e != hipSuccess) throw Error(std::string("hip_memcpy: ") + hipGetErrorString(e));
+    });
+    m.def("hip_stream_sync", [](uintptr_t stream) {
+        py::gil_scoped_release nogil;
+        hipError_t e = hipStreamSynchronize((hipStream_t)stream);
+        if (e != hipSuccess) throw Error(std::string("hip_stream_sync: ") + hipGetErrorString(e));
     });
     m.def("device_count", []() {
         int n = 0;

@@ -39,8 +39,6 @@ namespace {
 
 constexpr int kThreads = 256;
 constexpr int kWaves = kThreads / 64;
-constexpr int kRows = 4;                 // rows per lane in k_march
-constexpr int kTJ = kWaves * kRows;      // tile rows (j)
 constexpr int kTK = 64;                  // tile columns (k) = one wave64
 constexpr int kLW = kTK + 2;             // LDS row incl. k halos
 constexpr int kNaiveTJ = kWaves;         // naive kernel: one row per wave
@@ -147,8 +145,17 @@ __device__ __forceinline__ void store_point(const StepParams<T>& p, int i, int j
 
 // ---------------------------------------------------------------------------------------
 // 2.5-D marching kernel (LDS tile + register-rolling i column).
-template <class T, bool FIRST>
+template <class T>
+__device__ __forceinline__ T ld_stream(const T* p, bool nt) {
+    return nt ? __builtin_nontemporal_load(p) : *p;
+}
+
+// R = rows (j) per lane; the workgroup tile is (4R) x 64. NT = non-temporal loads of the
+// read-once level u^{n-2}.
+template <class T, bool FIRST, int R, bool NT>
 __global__ void __launch_bounds__(kThreads) k_march(const StepParams<T> p) {
+    constexpr int kRows = R;
+    constexpr int kTJ = kWaves * R;
     __shared__ T lds[2][kTJ + 2][kLW];
 
     const int bid = blockIdx.x;
@@ -218,7 +225,7 @@ __global__ void __launch_bounds__(kThreads) k_march(const StepParams<T> p) {
         Pv[r] = ld_ok[r] ? u1[i64(ib - 1) * si + rowoff[r]] : T(0);
         Cv[r] = ld_ok[r] ? u1[i64(ib) * si + rowoff[r]] : T(0);
         Nv[r] = ld_ok[r] ? u1[i64(ib + 1) * si + rowoff[r]] : T(0);
-        U2c[r] = (!FIRST && valid[r]) ? u2[i64(ib) * si + rowoff[r]] : T(0);
+        U2c[r] = (!FIRST && valid[r]) ? ld_stream(u2 + i64(ib) * si + rowoff[r], NT) : T(0);
     }
     T H = hon ? u1[i64(ib) * si + hoff] : T(0);
 
@@ -232,7 +239,7 @@ __global__ void __launch_bounds__(kThreads) k_march(const StepParams<T> p) {
 #pragma unroll
         for (int r = 0; r < kRows; ++r) {
             NN[r] = (more && ld_ok[r]) ? u1[i64(i + 2) * si + rowoff[r]] : T(0);
-            U2n[r] = (!FIRST && more && valid[r]) ? u2[i64(i + 1) * si + rowoff[r]] : T(0);
+            U2n[r] = (!FIRST && more && valid[r]) ? ld_stream(u2 + i64(i + 1) * si + rowoff[r], NT) : T(0);
         }
         if (more && hon) Hn = u1[i64(i + 1) * si + hoff];
 
@@ -285,7 +292,8 @@ __global__ void __launch_bounds__(kThreads) k_naive(const StepParams<T> p) {
     const int tk = local % B.tiles_k;
     local /= B.tiles_k;
     const int tj = local % B.tiles_j;
-    const int i = B.i0 + local / B.tiles_j;  // chunk == 1
+    const int ib = B.i0 + (local / B.tiles_j) * B.chunk;
+    const int ie = min(B.i1, ib + B.chunk - 1);
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int k = B.kbase + tk * kTK + lane;
     const int j = B.j0 + tj * kNaiveTJ + w;
@@ -294,37 +302,46 @@ __global__ void __launch_bounds__(kThreads) k_naive(const StepParams<T> p) {
     if (k >= B.k0 && k <= B.k1 && j <= B.j1) {
         const i64 si = p.si;
         const int rowoff = j * p.sj + k;
-        const i64 o = i64(i) * si + rowoff;
-        const T c = p.u1[o];
-        const T lap = laplace7(c, p.u1[o - si], p.u1[o + si], p.u1[o - p.sj], p.u1[o + p.sj],
-                               p.u1[o - 1], p.u1[o + 1], p.hx2, p.hy2, p.hz2);
-        const T v = FIRST ? taylor_first(c, lap, p.coef) : leapfrog(c, p.u2[o], lap, p.coef);
-        store_point(p, i, j, k, o, rowoff, v);
-        bad = nonfinite(v);
-        if (i >= p.ei0 && i <= p.ei1)
-            accumulate_error(v, analytic(p.tx[i], p.ty[j], p.tz[k], p.ct), ma, mr);
+        const T tyj = p.ty[j], tzk = p.tz[k];
+        for (int i = ib; i <= ie; ++i) {
+            const i64 o = i64(i) * si + rowoff;
+            const T c = p.u1[o];
+            const T lap = laplace7(c, p.u1[o - si], p.u1[o + si], p.u1[o - p.sj],
+                                   p.u1[o + p.sj], p.u1[o - 1], p.u1[o + 1], p.hx2, p.hy2, p.hz2);
+            const T v = FIRST ? taylor_first(c, lap, p.coef) : leapfrog(c, p.u2[o], lap, p.coef);
+            store_point(p, i, j, k, o, rowoff, v);
+            bad |= nonfinite(v);
+            if (i >= p.ei0 && i <= p.ei1)
+                accumulate_error(v, analytic(p.tx[i], tyj, tzk, p.ct), ma, mr);
+        }
     }
     commit_errors(ma, mr, bad, p.err);
 }
 
 // ---------------------------------------------------------------------------------------
+// Layer 0 (initial condition): one workgroup per 4 x 64 (j,k) tile and `chunk` planes.
 template <class T>
-__global__ void __launch_bounds__(kThreads) k_init(T* u, i64 si, int sj, Box bx, int ws0,
-                                                   int wd0, int ws1, int wd1, const T* tx,
-                                                   const T* ty, const T* tz, T ct, u64* err) {
+__global__ void __launch_bounds__(kThreads) k_init(T* u, i64 si, int sj, Box bx, int chunk,
+                                                   int ws0, int wd0, int ws1, int wd1,
+                                                   const T* tx, const T* ty, const T* tz, T ct,
+                                                   u64* err) {
     const int k = bx.k0 + blockIdx.x * 64 + (threadIdx.x & 63);
     const int j = bx.j0 + blockIdx.y * kWaves + (threadIdx.x >> 6);
-    const int i = bx.i0 + blockIdx.z;
+    const int ib = bx.i0 + blockIdx.z * chunk;
+    const int ie = min(bx.i1, ib + chunk - 1);
     T ma = T(kErrInit), mr = T(kErrInit);
     bool bad = false;
     if (k <= bx.k1 && j <= bx.j1) {
         const int rowoff = j * sj + k;
-        const T f = analytic(tx[i], ty[j], tz[k], ct);
-        u[i64(i) * si + rowoff] = f;
-        if (i == ws0) u[i64(wd0) * si + rowoff] = f;
-        if (i == ws1) u[i64(wd1) * si + rowoff] = f;
-        bad = nonfinite(f);
-        accumulate_error(f, analytic(tx[i], ty[j], tz[k], ct), ma, mr);
+        const T tyj = ty[j], tzk = tz[k];
+        for (int i = ib; i <= ie; ++i) {
+            const T f = analytic(tx[i], tyj, tzk, ct);
+            u[i64(i) * si + rowoff] = f;
+            if (i == ws0) u[i64(wd0) * si + rowoff] = f;
+            if (i == ws1) u[i64(wd1) * si + rowoff] = f;
+            bad |= nonfinite(f);
+            accumulate_error(f, analytic(tx[i], tyj, tzk, ct), ma, mr);
+        }
     }
     commit_errors(ma, mr, bad, err);
 }
@@ -355,7 +372,9 @@ __global__ void k_faces(T* u, i64 si, int sj, int ny, int nz, FaceOps<T> ops, bo
     const int i = 1 + blockIdx.y;
     const int t = blockIdx.x * blockDim.x + threadIdx.x;
     const int len = f.axis == 1 ? nz : ny;
-    if (t >= len) return;
+    // ghost corners/edges are never read by the 7-point stencil: skipping them keeps the
+    // y and z faces of one launch from writing the same cells
+    if (t < 1 || t > len - 2) return;
     T* g = f.axis == 1 ? u + i64(i) * si + i64(f.index) * sj + t
                        : u + i64(i) * si + i64(t) * sj + f.index;
     T* q = f.buf + i64(i - 1) * len + t;
@@ -377,10 +396,43 @@ inline int cdiv(int a, int b) { return (a + b - 1) / b; }
 
 }  // namespace
 
-int march_rows_per_thread() { return kRows; }
+int march_rows_per_thread() { return 4; }
+
+KernelVariant parse_kernel_variant(const std::string& name) {
+    KernelVariant v;
+    if (name == "naive") {
+        v.march = false;
+        return v;
+    }
+    if (name == "auto" || name == "march" || name == "march4") return v;
+    if (name == "march2") v.rows = 2;
+    else if (name == "march8") v.rows = 8;
+    else if (name == "march4nt") v.nt = true;
+    else if (name == "march2nt") v.rows = 2, v.nt = true;
+    else if (name == "march8nt") v.rows = 8, v.nt = true;
+    else throw Error("wave3d: unknown kernel variant " + name);
+    return v;
+}
+
+std::string kernel_variant_name(const KernelVariant& v) {
+    if (!v.march) return "naive";
+    return "march" + std::to_string(v.rows) + (v.nt ? "nt" : "");
+}
+
+template <class T, bool FIRST>
+static void (*march_kernel(const KernelVariant& v))(const StepParams<T>) {
+    switch (v.rows * 2 + (v.nt ? 1 : 0)) {
+        case 4: return k_march<T, FIRST, 2, false>;
+        case 5: return k_march<T, FIRST, 2, true>;
+        case 9: return k_march<T, FIRST, 4, true>;
+        case 16: return k_march<T, FIRST, 8, false>;
+        case 17: return k_march<T, FIRST, 8, true>;
+        default: return k_march<T, FIRST, 4, false>;
+    }
+}
 
 template <class T>
-void launch_step(StepKernel kind, bool first, const T* u1, const T* u2, T* u, const GridView& gv,
+void launch_step(const KernelVariant& kind, bool first, const T* u1, const T* u2, T* u, const GridView& gv,
                  const Box* boxes, int nbox, int ei0, int ei1, const Wrap& wrap,
                  const FusedPack<T>& pack, const T* tx, const T* ty, const T* tz,
                  const StepCoefs& c, u64* err, int chunk, hipStream_t s) {
@@ -418,8 +470,8 @@ void launch_step(StepKernel kind, bool first, const T* u1, const T* u2, T* u, co
     p.coef = T(c.coef);
     p.ct = T(c.ct);
     p.err = err;
-    const bool march = kind == StepKernel::March;
-    const int tj_rows = march ? kTJ : kNaiveTJ;
+    const bool march = kind.march;
+    const int tj_rows = march ? kWaves * kind.rows : kNaiveTJ;
     int nb = 0, total = 0;
     for (int q = 0; q < nbox; ++q) {
         const Box& bx = boxes[q];
@@ -435,7 +487,7 @@ void launch_step(StepKernel kind, bool first, const T* u1, const T* u2, T* u, co
         L.tiles_j = cdiv(bx.j1 - bx.j0 + 1, tj_rows);
         const int planes = bx.i1 - bx.i0 + 1;
         int ch = 1;
-        if (march) {
+        {
             if (chunk > 0) {
                 ch = std::min(chunk, planes);
             } else {
@@ -454,7 +506,7 @@ void launch_step(StepKernel kind, bool first, const T* u1, const T* u2, T* u, co
     p.nbox = nb;
     if (nb == 0) return;
     void (*kern)(const StepParams<T>);
-    if (march) kern = first ? k_march<T, true> : k_march<T, false>;
+    if (march) kern = first ? march_kernel<T, true>(kind) : march_kernel<T, false>(kind);
     else kern = first ? k_naive<T, true> : k_naive<T, false>;
     hipLaunchKernelGGL(kern, dim3(total), dim3(kThreads), 0, s, p);
     HIP_OK(hipGetLastError());
@@ -466,8 +518,11 @@ void launch_init(T* u, const GridView& gv, const Box& bx, const Wrap& wrap, cons
     if (bx.empty()) return;
     W3D_REQUIRE(bx.i0 >= 1 && bx.i1 <= gv.nx - 2 && bx.j1 <= gv.ny - 2 && bx.k1 <= gv.nz - 2,
                 "init box outside the owned region");
-    dim3 grid(cdiv(bx.k1 - bx.k0 + 1, 64), cdiv(bx.j1 - bx.j0 + 1, kWaves), bx.i1 - bx.i0 + 1);
-    hipLaunchKernelGGL(k_init<T>, grid, dim3(kThreads), 0, s, u, gv.si, gv.sj, bx, wrap.src[0],
+    const int planes = bx.i1 - bx.i0 + 1;
+    const int tiles = cdiv(bx.k1 - bx.k0 + 1, 64) * cdiv(bx.j1 - bx.j0 + 1, kWaves);
+    const int chunk = std::min(planes, std::max(1, cdiv(planes * tiles, 4096 * 4)));
+    dim3 grid(cdiv(bx.k1 - bx.k0 + 1, 64), cdiv(bx.j1 - bx.j0 + 1, kWaves), cdiv(planes, chunk));
+    hipLaunchKernelGGL(k_init<T>, grid, dim3(kThreads), 0, s, u, gv.si, gv.sj, bx, chunk, wrap.src[0],
                        wrap.dst[0], wrap.src[1], wrap.dst[1], tx, ty, tz, T(ct0), err);
     HIP_OK(hipGetLastError());
 }
@@ -507,7 +562,7 @@ void launch_encode_keys(const double* v, u64* k, int n, hipStream_t s) {
 }
 
 #define W3D_INST(T)                                                                          \
-    template void launch_step<T>(StepKernel, bool, const T*, const T*, T*, const GridView&,  \
+    template void launch_step<T>(const KernelVariant&, bool, const T*, const T*, T*, const GridView&,  \
                                  const Box*, int, int, int, const Wrap&, const FusedPack<T>&, \
                                  const T*, const T*, const T*, const StepCoefs&, u64*, int,   \
                                  hipStream_t);                                               \

@@ -8,6 +8,8 @@
 
 #include <hip/hip_runtime.h>
 
+#include <string>
+
 #include "common.hpp"
 
 namespace wave3d {
@@ -44,12 +46,20 @@ struct Wrap {
     int dst[2] = {-1, -1};
 };
 
-enum class StepKernel { March, Naive };
+// Stencil kernel variant: 2.5-D marching (rows per lane, non-temporal u^{n-2} loads) or
+// the one-point-per-lane kernel.
+struct KernelVariant {
+    bool march = true;
+    int rows = 4;
+    bool nt = false;
+};
+KernelVariant parse_kernel_variant(const std::string& name);
+std::string kernel_variant_name(const KernelVariant& v);
 
 // One time layer n >= 1 over `nbox` boxes. Errors are accumulated for i in [ei0, ei1]
 // into err[0..2] = {abs key, rel key, nonfinite flag}.
 template <class T>
-void launch_step(StepKernel kind, bool first, const T* u1, const T* u2, T* u, const GridView& gv,
+void launch_step(const KernelVariant& kind, bool first, const T* u1, const T* u2, T* u, const GridView& gv,
                  const Box* boxes, int nbox, int ei0, int ei1, const Wrap& wrap,
                  const FusedPack<T>& pack, const T* tx, const T* ty, const T* tz,
                  const StepCoefs& c, u64* err, int chunk, hipStream_t s);

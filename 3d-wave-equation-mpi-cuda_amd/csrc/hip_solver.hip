@@ -68,9 +68,8 @@ public:
             world_ = std::max(1, c.ranks);
             for (int r = 0; r < world_; ++r) local_.push_back(r);
         }
-        if (c.kernel == "naive") kind_ = StepKernel::Naive;
-        else if (c.kernel == "auto" || c.kernel == "march") kind_ = StepKernel::March;
-        else throw Error("wave3d: unknown --kernel " + c.kernel);
+        kind_ = parse_kernel_variant(c.kernel);
+        naive_.march = false;
         // interior/shell split + comm stream whenever there is a remote halo to hide
         overlap_ = c.overlap && (ext_ != nullptr || world_ > 1);
     }
@@ -94,7 +93,7 @@ public:
         res.Np = world_;
         res.dtype = cfg_.dtype;
         res.backend = "hip";
-        res.kernel = kind_ == StepKernel::March ? "march" : "naive";
+        res.kernel = kernel_variant_name(kind_);
         res.courant = prob_.courant;
         res.transport = ext_ ? ext_->name() : (world_ > 1 ? "loopback" : "self");
         for (int a = 0; a < 3; ++a) res.dims[a] = ranks_[0].topo.dims[a];
@@ -257,7 +256,7 @@ private:
         return c;
     }
 
-    void step_boxes(DevRank<T>& R, int n, const Box* boxes, int nbox, StepKernel kind,
+    void step_boxes(DevRank<T>& R, int n, const Box* boxes, int nbox, const KernelVariant& kind,
                     hipStream_t s) {
         const T* u1 = R.g[(n + 2) % 3];
         const T* u2 = R.g[(n + 1) % 3];
@@ -389,7 +388,7 @@ private:
                 HIP_CHECK(hipStreamWaitEvent(s_comp_, ev_halo_, 0));
                 for (auto& R : ranks_)
                     if (!R.shell.empty())
-                        step_boxes(R, n, R.shell.data(), int(R.shell.size()), StepKernel::Naive,
+                        step_boxes(R, n, R.shell.data(), int(R.shell.size()), naive_,
                                    s_comp_);
             } else {
                 for (auto& R : ranks_) step_boxes(R, n, &R.compute, 1, kind_, s_comp_);
@@ -572,7 +571,7 @@ private:
     Transport* ext_;
     Problem prob_;
     FaultSpec fault_;
-    StepKernel kind_ = StepKernel::March;
+    KernelVariant kind_, naive_;
     bool overlap_ = false;
     int world_ = 1;
     std::vector<int> local_;

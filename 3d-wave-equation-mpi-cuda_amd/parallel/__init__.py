@@ -9,7 +9,7 @@ from .topology import dims_create, topology  # noqa: F401
 
 def __getattr__(name):
     if name in ("init_from_env", "rccl_transport", "TorchHostTransport", "env_rank",
-                "broadcast_bytes"):
+                "broadcast_bytes", "TorchStagedTransport", "make_transport"):
         from . import dist as _d
 
         return getattr(_d, name)

@@ -8,6 +8,10 @@
 * :class:`TorchHostTransport` — a host-memory transport over torch.distributed point-to-
   point (gloo), used by the OpenMP backend for multi-process CPU runs and tests; it is the
   process-level equivalent of the reference's MPI_Sendrecv chain (mpi_new.cpp:201-238).
+* :class:`TorchStagedTransport` — a *device* transport that stages faces through host
+  memory over gloo. Slow, but lets P processes share one GPU (RCCL refuses duplicate GPUs),
+  which is how the multi-process HIP path is tested on a single MI355X — the role MPS
+  oversubscription plays in the reference (README.txt:44, cuda_sol.cpp:519).
 """
 from __future__ import annotations
 
@@ -28,10 +32,11 @@ def env_rank() -> tuple[int, int, int]:
     return r, w, lr
 
 
-def init_from_env(backend: str | None = None) -> tuple[int, int, int]:
-    """Initialise the default process group from torchrun-style env (idempotent)."""
+def init_from_env(backend: str | None = None, force: bool = False) -> tuple[int, int, int]:
+    """Initialise the default process group from torchrun-style env (idempotent).
+    A single-process world is only initialised with ``force`` (no group is needed)."""
     rank, world, local = env_rank()
-    if world > 1 and not dist.is_initialized():
+    if (world > 1 or force) and not dist.is_initialized():
         if backend is None:
             backend = "nccl" if torch.cuda.is_available() else "gloo"
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
@@ -117,3 +122,72 @@ class TorchHostTransport:
                 dist.barrier(group=self.g)
 
         return _T(group)
+
+
+class TorchStagedTransport:
+    """Factory for a device ``Transport``: D2H -> gloo p2p -> H2D (testing/bring-up only)."""
+
+    def __new__(cls, group=None):
+        C = load()
+
+        class _S(C.Transport):
+            def __init__(self, g):
+                C.Transport.__init__(self)
+                self.g = g
+
+            def name(self):
+                return "staged." + dist.get_backend(self.g)
+
+            def rank(self):
+                return dist.get_rank(self.g)
+
+            def size(self):
+                return dist.get_world_size(self.g)
+
+            def device(self):
+                return True
+
+            def exchange(self, sends, recvs, stream):
+                C.hip_stream_sync(stream)
+                sbufs = []
+                for peer, tag, addr, nb in sends:
+                    h = np.empty(nb, dtype=np.uint8)
+                    C.hip_memcpy(h.ctypes.data, addr, nb, stream)
+                    sbufs.append((peer, tag, torch.from_numpy(h)))
+                rbufs = [(addr, nb, torch.empty(nb, dtype=torch.uint8)) for _, _, addr, nb in recvs]
+                ops = [dist.irecv(t, src=peer, group=self.g, tag=tag)
+                       for (peer, tag, _, _), (_, _, t) in zip(recvs, rbufs)]
+                ops += [dist.isend(t, dst=peer, group=self.g, tag=tag) for peer, tag, t in sbufs]
+                for w in ops:
+                    w.wait()
+                for addr, nb, t in rbufs:
+                    C.hip_memcpy(addr, t.numpy().ctypes.data, nb, stream)
+
+            def allreduce_max_u64(self, addr, n, stream):
+                h = np.empty(n, dtype=np.uint64)
+                C.hip_memcpy(h.ctypes.data, addr, n * 8, stream)
+                t = torch.from_numpy((h ^ _SIGN).view(np.int64).copy())
+                dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.g)
+                out = t.numpy().view(np.uint64) ^ _SIGN
+                C.hip_memcpy(addr, out.ctypes.data, n * 8, stream)
+
+            def allreduce_max_host(self, values):
+                t = torch.tensor(values, dtype=torch.float64)
+                dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.g)
+                return t.tolist()
+
+            def barrier(self):
+                dist.barrier(group=self.g)
+
+        return _S(group)
+
+
+def make_transport(kind: str, backend: str = "hip"):
+    """'rccl' (native, one GPU per rank), 'staged' (device via gloo), 'gloo' (host, CPU)."""
+    if kind == "rccl":
+        return rccl_transport(torch.cuda.current_device())
+    if kind == "staged":
+        return TorchStagedTransport()
+    if kind in ("gloo", "host"):
+        return TorchHostTransport()
+    raise ValueError(f"unknown transport {kind}")

@@ -1,0 +1,87 @@
+"""CLI parsing (C03) and the reference-format output of the programs (Appendix A)."""
+import os
+import subprocess
+
+import pytest
+
+
+def test_parse_positionals_and_pi(C):
+    d = C.parse(["32", "4", "pi", "1.5", "pi"])
+    assert d["N"] == 32 and d["Np"] == 4 and d["T"] == 1.0 and d["timesteps"] == 20
+    assert d["Lx"] == 3.1415926535 and d["Ly"] == 1.5 and d["pi"] == 3.1415926535
+    d = C.parse(["64", "1", "1", "1", "1", "2.5", "50", "--pi", "exact", "--dtype", "fp32"])
+    assert d["T"] == 2.5 and d["timesteps"] == 50 and d["dtype"] == "fp32"
+    assert abs(d["pi"] - 3.141592653589793) < 1e-15
+    assert d["tau"] == 2.5 / 50
+
+
+@pytest.mark.parametrize("bad", [["32", "1", "pi", "pi"], ["x", "1", "pi", "pi", "pi"],
+                                 ["32", "1", "pi", "pi", "pi", "1", "20", "--bogus"],
+                                 ["32", "1", "pi", "pi", "-1"], ["32", "1", "pi", "pi", "pi", "--dims", "2,2"]])
+def test_parse_errors(C, bad):
+    with pytest.raises(Exception):
+        C.parse(bad)
+
+
+def test_constants_match_reference_formulas(C):
+    import math
+
+    d = C.parse(["128", "1", "pi", "pi", "pi", "1", "20"])
+    PI = 3.1415926535
+    assert d["a2"] == 1 / (4 * PI * PI)
+    assert d["a_t"] == 0.5 * math.sqrt(4 / (PI * PI) + 1 / (PI * PI) + 1 / (PI * PI))
+    assert d["hx"] == PI / 128 and d["tau"] == 1 / 20
+    assert abs(d["courant"] - 0.324228) < 1e-6  # survey golden C for N=128,K=20
+
+
+def test_cpu_program_output_byte_identical(cpu_prog, tmp_path):
+    """`wave3d_cpu 32 4 pi pi pi 1 20` reproduces the reference's error table (Appendix C.1)."""
+    from wave3d.utils import GOLDEN_N32_K20
+
+    out = subprocess.run([cpu_prog, "32", "4", "pi", "pi", "pi", "1", "20"], cwd=tmp_path,
+                         capture_output=True, text=True, timeout=60)
+    assert out.returncode == 0
+    assert out.stdout.startswith("C = 0.0810569\n")
+    text = open(tmp_path / "output_N32_Np4.txt").read().splitlines()
+    assert text[0].startswith("numerical solution calculated in ")
+    want = [f"max abs and rel errors on layer {n}: {a} {r}" for n, (a, r) in enumerate(GOLDEN_N32_K20)]
+    assert text[1:] == want
+
+
+def test_cpu_program_mpi_format_with_ranks(cpu_prog, tmp_path):
+    out = subprocess.run([cpu_prog, "32", "1", "pi", "pi", "pi", "1", "20", "--ranks", "8",
+                          "--format", "new"], cwd=tmp_path, capture_output=True, text=True, timeout=60)
+    assert out.returncode == 0
+    assert out.stdout.count("local size = 8") == 8
+    lines = open(tmp_path / "output_N32_Np1.txt").read().splitlines()
+    assert lines[0].startswith("grids initialized in ")
+    assert lines[-2].startswith("total MPI exchange time: ") and lines[-1].startswith("total loop time: ")
+    assert lines[-3] == "max abs and rel errors on layer 20: 0.000175963 0.000194911"
+
+
+def test_cuda_format(cpu_prog, tmp_path):
+    subprocess.run([cpu_prog, "32", "1", "pi", "pi", "pi", "1", "20", "--format", "cuda",
+                    "--out-name", "c.txt", "--quiet"], cwd=tmp_path, check=True, timeout=60)
+    lines = open(tmp_path / "c.txt").read().splitlines()
+    assert lines[0].startswith("initialization done in ")
+    assert [l.split(":")[0] for l in lines[-4:]] == [
+        "total host-device exchange time", "total loop time", "total MPI exchange time",
+        "total error calculation time"]
+    assert all(l.endswith(" ms") for l in lines[-4:])
+
+
+def test_strict_cfl_refuses(cpu_prog, tmp_path):
+    out = subprocess.run([cpu_prog, "512", "1", "pi", "pi", "pi", "1", "20", "--strict-cfl"],
+                         cwd=tmp_path, capture_output=True, text=True, timeout=60)
+    assert out.returncode == 2 and "Courant" in out.stderr
+
+
+def test_json_summary(cpu_prog, tmp_path):
+    import json
+
+    out = subprocess.run([cpu_prog, "16", "2", "pi", "pi", "pi", "1", "10", "--json", "--quiet",
+                          "--format", "none"], cwd=tmp_path, capture_output=True, text=True, timeout=60)
+    d = json.loads(out.stdout.strip().splitlines()[-1])
+    assert d["N"] == 16 and d["timesteps"] == 10 and d["backend"] == "cpu"
+    assert d["linf_abs"] > 0 and d["mpts_per_s"] > 0
+    assert not os.path.exists(tmp_path / "output_N16_Np2.txt")

@@ -1,0 +1,125 @@
+"""OpenMP oracle: goldens (Appendix C), decomposition invariance, bitwise agreement with the
+plain-PyTorch solve, fp32, checkpoint/resume, fault detection."""
+import pytest
+
+
+def _solve(prob, **kw):
+    import wave3d
+
+    kw.setdefault("threads", 4)
+    return wave3d.WaveSolver(prob, "cpu", **kw).run()
+
+
+def _fmt(r):
+    from wave3d.utils import fmt6
+
+    return [(fmt6(a), fmt6(b)) for a, b in zip(r.max_abs, r.max_rel)]
+
+
+@pytest.mark.parametrize("ranks", [0, 2, 4, 8])
+def test_golden_table_n32(C, ranks):
+    import wave3d
+    from wave3d.utils import GOLDEN_N32_K20
+
+    assert _fmt(_solve(wave3d.WaveProblem(32, timesteps=20), ranks=ranks)) == GOLDEN_N32_K20
+
+
+@pytest.mark.parametrize("key", [(64, 20), (128, 20)])
+def test_golden_final(C, key):
+    import wave3d
+    from wave3d.utils import GOLDEN_FINAL
+
+    N, K = key
+    assert _fmt(_solve(wave3d.WaveProblem(N, timesteps=K), threads=8))[-1] == GOLDEN_FINAL[key]
+
+
+def test_spot_values(C):
+    import wave3d
+    from wave3d.utils import GOLDEN_SPOTS
+
+    for (N, K, ic), spots in GOLDEN_SPOTS.items():
+        if N > 128:
+            continue
+        got = _fmt(_solve(wave3d.WaveProblem(N, timesteps=K, ic=ic), threads=8))
+        for layer, v in spots.items():
+            assert got[layer] == v
+
+
+@pytest.mark.parametrize("ranks,dims", [(2, None), (3, None), (4, None), (6, None), (8, None),
+                                        (4, (1, 2, 2)), (4, (1, 1, 4)), (2, (1, 2, 1))])
+def test_decomposition_invariance(C, ranks, dims):
+    """The shifted IC exercises the periodic seams; every decomposition,
+    including dims[0]=1 (local periodic wrap) must give identical per-layer errors."""
+    import wave3d
+
+    p = wave3d.WaveProblem(27, Lx=1.3, Ly="pi", Lz=2.1, timesteps=11, ic="shifted")
+    base = _solve(p)
+    r = _solve(p, ranks=ranks, dims=dims)
+    assert r.max_abs == base.max_abs and r.max_rel == base.max_rel
+
+
+def test_bitwise_equal_to_torch_reference(C):
+    import wave3d
+    from wave3d.ops import reference
+
+    for ic, phase in (("ref", 0.0), ("shifted", 0.7)):
+        r = _solve(wave3d.WaveProblem(24, Lx=1.1, Ly="pi", Lz=1.9, timesteps=9, ic=ic))
+        a, b, _ = reference.solve(24, 9, L=(1.1, "pi", 1.9), phase=phase)
+        assert r.max_abs == a and r.max_rel == b
+
+
+def test_fp32_close_to_fp64(C):
+    import wave3d
+
+    a = _solve(wave3d.WaveProblem(48, timesteps=20))
+    b = _solve(wave3d.WaveProblem(48, timesteps=20, dtype="fp32"))
+    assert b.dtype == "fp32"
+    assert b.max_abs[-1] == pytest.approx(a.max_abs[-1], rel=0.05)
+
+
+def test_checkpoint_resume_bitwise(C, tmp_path):
+    import wave3d
+
+    p = wave3d.WaveProblem(20, timesteps=14, ic="shifted")
+    full = _solve(p, ranks=4)
+    _solve(p, ranks=4, checkpoint_every=6, checkpoint_dir=str(tmp_path))
+    res = _solve(p, ranks=4, resume=str(tmp_path))
+    assert res.extra["resumed_from"] == 12
+    assert res.max_abs == full.max_abs and res.max_rel == full.max_rel
+    # a different configuration is refused
+    with pytest.raises(Exception):
+        _solve(wave3d.WaveProblem(20, timesteps=15), ranks=4, resume=str(tmp_path))
+
+
+def test_fault_injection_detected(C):
+    import wave3d
+
+    p = wave3d.WaveProblem(16, timesteps=10)
+    r = _solve(p, check_every=1, fault="nan:0:3")
+    assert r.aborted and r.abort_layer == 4 and "non-finite" in r.abort_reason
+    clean = _solve(p, ranks=2)
+    bad = _solve(p, ranks=2, fault="drop_face:1:4")
+    assert bad.max_abs[-1] > 10 * clean.max_abs[-1]
+
+
+def test_divergence_abort(C):
+    import wave3d
+
+    # C = 1.3 > 1/sqrt(3): the reference silently reports 6.9e7
+    p = wave3d.WaveProblem(64, timesteps=20, T=8.0)
+    assert p.courant > 1.2
+    r = _solve(p, check_every=1)
+    assert r.aborted
+
+
+def test_reference_laplacian_exact_on_quadratics():
+    import torch
+
+    from wave3d.ops import reference
+
+    n = 9
+    x = torch.arange(n, dtype=torch.float64)
+    X, Y, Z = torch.meshgrid(x, x, x, indexing="ij")
+    u = 0.5 * X * X + 1.5 * Y * Y - Z * Z + 3 * X * Y
+    lap = reference.laplace7(u, 1.0, 1.0, 1.0)
+    assert torch.allclose(lap, torch.full_like(lap, 1.0 + 3.0 - 2.0), atol=1e-12)

@@ -1,0 +1,67 @@
+"""Multi-process runs through torch.distributed.run (the launcher the benchmark uses).
+
+CPU: OpenMP backend, gloo host transport, world 2/4/8.
+GPU (marked): HIP backend with P processes sharing one MI355X through the staged device
+transport (the reference's MPS-oversubscription test mode, P5), with and without the
+interior/shell overlap; and the native RCCL transport in a single-rank world.
+"""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def torchrun(nproc, flags, args, timeout=300):
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_port()),
+           os.path.join(ROOT, "tools", "dist_solve.py")] + flags + ["--"] + args
+    env = dict(os.environ, OMP_NUM_THREADS="1")
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, env=env, cwd=ROOT)
+    assert out.returncode == 0, out.stdout[-3000:] + out.stderr[-3000:]
+    line = [l for l in out.stdout.splitlines() if l.startswith("RESULT ")]
+    assert line, out.stdout[-2000:] + out.stderr[-2000:]
+    return json.loads(line[0][7:])
+
+
+ARGS = ["27", "1", "1.3", "pi", "2.1", "1", "11", "--ic", "shifted", "--threads", "1"]
+
+
+@pytest.fixture(scope="module")
+def single_cpu(C):
+    return C.run(ARGS, "cpu", None, False, True)
+
+
+@pytest.mark.parametrize("P", [2, 4, 8])
+def test_cpu_gloo_matches_single_process(C, single_cpu, P):
+    r = torchrun(P, ["--backend", "cpu", "--transport", "gloo"], ARGS)
+    assert r["nprocs"] == P and r["transport"] == "torch.gloo"
+    assert r["max_abs"] == single_cpu["max_abs"] and r["max_rel"] == single_cpu["max_rel"]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("P,overlap", [(2, True), (4, True), (8, True), (2, False), (4, False)])
+def test_hip_multiprocess_shared_gpu(C, single_cpu, P, overlap):
+    extra = [] if overlap else ["--no-overlap"]
+    r = torchrun(P, ["--backend", "hip", "--transport", "staged", "--shared-device"], ARGS + extra)
+    assert r["nprocs"] == P and r["transport"] == "staged.gloo"
+    assert r["max_abs"] == single_cpu["max_abs"] and r["max_rel"] == single_cpu["max_rel"]
+
+
+@pytest.mark.gpu
+def test_rccl_transport_single_rank(C, single_cpu):
+    r = torchrun(1, ["--backend", "hip", "--transport", "rccl"], ARGS)
+    assert r["transport"] == "rccl"
+    assert r["max_abs"] == single_cpu["max_abs"] and r["max_rel"] == single_cpu["max_rel"]
