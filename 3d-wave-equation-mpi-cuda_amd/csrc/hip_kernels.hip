@@ -73,6 +73,7 @@ struct StepParams {
     const T* ty;
     const T* tz;
     T hx2, hy2, hz2, coef, ct;
+    T rx2, ry2, rz2;  // 1/h^2 (fast-math variants only)
     u64* err;
 };
 
@@ -152,7 +153,7 @@ __device__ __forceinline__ T ld_stream(const T* p, bool nt) {
 
 // R = rows (j) per lane; the workgroup tile is (4R) x 64. NT = non-temporal loads of the
 // read-once level u^{n-2}.
-template <class T, bool FIRST, int R, bool NT>
+template <class T, bool FIRST, int R, bool NT, bool FAST = false>
 __global__ void __launch_bounds__(kThreads) k_march(const StepParams<T> p) {
     constexpr int kRows = R;
     constexpr int kTJ = kWaves * R;
@@ -258,13 +259,23 @@ __global__ void __launch_bounds__(kThreads) k_march(const StepParams<T> p) {
             const T jp = r == kRows - 1 ? lds[buf][lr + 1][1 + lane] : Cv[r + 1];
             const T km = lds[buf][lr][lane];
             const T kp = lds[buf][lr][lane + 2];
-            const T lap = laplace7(Cv[r], Pv[r], Nv[r], jm, jp, km, kp, p.hx2, p.hy2, p.hz2);
-            const T v = FIRST ? taylor_first(Cv[r], lap, p.coef) : leapfrog(Cv[r], U2c[r], lap, p.coef);
+            T v;
+            if constexpr (FAST) {
+                const T lap = laplace7_fast(Cv[r], Pv[r], Nv[r], jm, jp, km, kp, p.rx2, p.ry2, p.rz2);
+                v = FIRST ? __builtin_fma(p.coef, lap, Cv[r])
+                          : __builtin_fma(p.coef, lap, T(2) * Cv[r] - U2c[r]);
+            } else {
+                const T lap = laplace7(Cv[r], Pv[r], Nv[r], jm, jp, km, kp, p.hx2, p.hy2, p.hz2);
+                v = FIRST ? taylor_first(Cv[r], lap, p.coef) : leapfrog(Cv[r], U2c[r], lap, p.coef);
+            }
             if (valid[r]) {
                 const int j = jt + w * kRows + r;
                 store_point(p, i, j, k, i64(i) * si + rowoff[r], rowoff[r], v);
                 bad |= nonfinite(v);
-                if (erow) accumulate_error(v, analytic(sx, ty[r], tz, p.ct), ma, mr);
+                if (erow) {
+                    if constexpr (FAST) accumulate_error_fast(v, analytic(sx, ty[r], tz, p.ct), ma, mr);
+                    else accumulate_error(v, analytic(sx, ty[r], tz, p.ct), ma, mr);
+                }
             }
         }
 #pragma unroll
@@ -404,23 +415,30 @@ KernelVariant parse_kernel_variant(const std::string& name) {
         v.march = false;
         return v;
     }
-    if (name == "auto" || name == "march" || name == "march4") return v;
+    if (name == "auto") {  // best measured single-step variant on MI355X (profiles/)
+        v.rows = 2;
+        return v;
+    }
+    if (name == "march" || name == "march4") return v;
     if (name == "march2") v.rows = 2;
     else if (name == "march8") v.rows = 8;
     else if (name == "march4nt") v.nt = true;
     else if (name == "march2nt") v.rows = 2, v.nt = true;
     else if (name == "march8nt") v.rows = 8, v.nt = true;
+    else if (name == "march2f") v.rows = 2, v.fast = true;
+    else if (name == "march4f") v.fast = true;
     else throw Error("wave3d: unknown kernel variant " + name);
     return v;
 }
 
 std::string kernel_variant_name(const KernelVariant& v) {
     if (!v.march) return "naive";
-    return "march" + std::to_string(v.rows) + (v.nt ? "nt" : "");
+    return "march" + std::to_string(v.rows) + (v.nt ? "nt" : "") + (v.fast ? "f" : "");
 }
 
 template <class T, bool FIRST>
 static void (*march_kernel(const KernelVariant& v))(const StepParams<T>) {
+    if (v.fast) return v.rows == 2 ? k_march<T, FIRST, 2, false, true> : k_march<T, FIRST, 4, false, true>;
     switch (v.rows * 2 + (v.nt ? 1 : 0)) {
         case 4: return k_march<T, FIRST, 2, false>;
         case 5: return k_march<T, FIRST, 2, true>;
@@ -469,6 +487,9 @@ void launch_step(const KernelVariant& kind, bool first, const T* u1, const T* u2
     p.hz2 = T(c.hz2);
     p.coef = T(c.coef);
     p.ct = T(c.ct);
+    p.rx2 = T(1.0 / c.hx2);
+    p.ry2 = T(1.0 / c.hy2);
+    p.rz2 = T(1.0 / c.hz2);
     p.err = err;
     const bool march = kind.march;
     const int tj_rows = march ? kWaves * kind.rows : kNaiveTJ;
@@ -491,11 +512,9 @@ void launch_step(const KernelVariant& kind, bool first, const T* u1, const T* u2
             if (chunk > 0) {
                 ch = std::min(chunk, planes);
             } else {
-                // aim at ~2 resident waves of workgroups over the 256 CUs
-                const int tiles = L.tiles_k * L.tiles_j;
-                const int want = std::max(1, 2048 / std::max(1, tiles));
-                ch = std::max(8, cdiv(planes, want));
-                ch = std::min(ch, planes);
+                // 32-plane work items (chunk sweep on MI355X, profiles/): enough workgroups
+                // to balance the 256 CUs, 2 extra prologue planes per 32 computed
+                ch = std::min(32, planes);
             }
         }
         L.chunk = ch;

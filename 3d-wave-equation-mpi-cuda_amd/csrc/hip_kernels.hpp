@@ -52,6 +52,7 @@ struct KernelVariant {
     bool march = true;
     int rows = 4;
     bool nt = false;
+    bool fast = false;  // reciprocal/FMA math: not bitwise-reproducible (benchmark ablation)
 };
 KernelVariant parse_kernel_variant(const std::string& name);
 std::string kernel_variant_name(const KernelVariant& v);

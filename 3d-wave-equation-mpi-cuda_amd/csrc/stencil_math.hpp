@@ -74,6 +74,23 @@ W3D_HD void accumulate_error(T u, T f, T& mabs, T& mrel) {
     if (er > mrel) mrel = er;
 }
 
+// ---- fast-math variants (not bitwise-reproducible: reciprocal multiplies, FMAs) --------
+template <class T>
+W3D_HD T laplace7_fast(T c, T xm, T xp, T ym, T yp, T zm, T zp, T rx2, T ry2, T rz2) {
+    T two_c = T(2) * c;
+    T ans = (zm + zp - two_c) * rz2;
+    ans = __builtin_fma(ym + yp - two_c, ry2, ans);
+    return __builtin_fma(xm + xp - two_c, rx2, ans);
+}
+
+template <class T>
+W3D_HD void accumulate_error_fast(T u, T f, T& mabs, T& mrel) {
+    T ea = absval(u - f);
+    T er = ea / absval(f);
+    if (ea > mabs) mabs = ea;
+    if (er > mrel) mrel = er;
+}
+
 // True for NaN and +-Inf (x - x is NaN exactly for those).
 template <class T>
 W3D_HD bool nonfinite(T x) {

@@ -21,13 +21,13 @@ def _fmt(r):
     return [(fmt6(a), fmt6(b)) for a, b in zip(r.max_abs, r.max_rel)]
 
 
-@pytest.mark.parametrize("kernel", ["march", "naive"])
+@pytest.mark.parametrize("kernel", ["march", "naive", "auto", "march8"])
 def test_golden_n32(C, kernel):
     import wave3d
     from wave3d.utils import GOLDEN_N32_K20
 
     r = _solve(wave3d.WaveProblem(32, timesteps=20), kernel=kernel)
-    assert r.backend == "hip" and r.kernel == ("march4" if kernel == "march" else kernel)
+    assert r.backend == "hip" and r.kernel == {"march": "march4", "auto": "march2"}.get(kernel, kernel)
     assert _fmt(r) == GOLDEN_N32_K20
 
 
