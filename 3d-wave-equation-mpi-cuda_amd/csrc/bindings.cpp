@@ -112,9 +112,10 @@ T* P(uintptr_t p) { return reinterpret_cast<T*>(p); }
 GridView gview(const std::vector<i64>& g) {
     W3D_REQUIRE(g.size() == 5, "grid view = (nx, ny, nz, sj, si)");
     GridView v;
-    v.nx = int(g[0]);
-    v.ny = int(g[1]);
-    v.nz = int(g[2]);
+    v.X = int(g[0]) - 2;
+    v.Y = int(g[1]) - 2;
+    v.Z = int(g[2]) - 2;
+    v.G = 1;
     v.sj = int(g[3]);
     v.si = g[4];
     return v;
@@ -125,6 +126,14 @@ Box tobox(const std::vector<int>& b) {
     return Box{b[0], b[1], b[2], b[3], b[4], b[5]};
 }
 
+// flat (src, dst, src, dst, ...) list of at most kMaxWrap pairs
+Wrap towrap(const std::vector<int>& v) {
+    W3D_REQUIRE(v.size() % 2 == 0 && v.size() <= 2 * kMaxWrap, "wrap = (src, dst, ...) pairs");
+    Wrap w;
+    for (size_t q = 0; q < v.size() / 2; ++q) w.src[q] = v[2 * q], w.dst[q] = v[2 * q + 1];
+    return w;
+}
+
 template <class T>
 void k_step(const std::string& kind, bool first, uintptr_t u1, uintptr_t u2, uintptr_t u,
             const std::vector<i64>& g, const std::vector<std::vector<int>>& boxes, int ei0,
@@ -133,8 +142,7 @@ void k_step(const std::string& kind, bool first, uintptr_t u1, uintptr_t u2, uin
             const std::vector<uintptr_t>& packbuf, const std::vector<int>& packidx) {
     std::vector<Box> bx;
     for (auto& b : boxes) bx.push_back(tobox(b));
-    Wrap w;
-    if (wrap.size() == 4) w.src[0] = wrap[0], w.dst[0] = wrap[1], w.src[1] = wrap[2], w.dst[1] = wrap[3];
+    Wrap w = towrap(wrap);
     FusedPack<T> fp;
     if (packbuf.size() == 4 && packidx.size() == 4) {
         fp.zbuf[0] = P<T>(packbuf[0]), fp.zbuf[1] = P<T>(packbuf[1]);
@@ -152,8 +160,7 @@ template <class T>
 void k_init(uintptr_t u, const std::vector<i64>& g, const std::vector<int>& box,
             const std::vector<int>& wrap, uintptr_t tx, uintptr_t ty, uintptr_t tz, double ct0,
             uintptr_t err, uintptr_t stream) {
-    Wrap w;
-    if (wrap.size() == 4) w.src[0] = wrap[0], w.dst[0] = wrap[1], w.src[1] = wrap[2], w.dst[1] = wrap[3];
+    Wrap w = towrap(wrap);
     launch_init<T>(P<T>(u), gview(g), tobox(box), w, P<T>(tx), P<T>(ty), P<T>(tz), ct0,
                    P<u64>(err), (hipStream_t)stream);
 }

@@ -34,11 +34,12 @@ std::string checkpoint_path(const std::string& dir, int rank) {
 
 namespace {
 
-void io_owned(std::fstream& f, char* base, int nx, int ny, int nz, int pitch, int es, bool write) {
-    const size_t row = size_t(nz - 2) * es;
-    for (int i = 1; i <= nx - 2; ++i)
-        for (int j = 1; j <= ny - 2; ++j) {
-            char* p = base + ((size_t(i) * ny + j) * pitch + 1) * es;
+void io_owned(std::fstream& f, const HostLevel& L, int es, bool write) {
+    const size_t row = size_t(L.Z) * es;
+    char* base = static_cast<char*>(L.origin);
+    for (int i = 1; i <= L.X; ++i)
+        for (int j = 1; j <= L.Y; ++j) {
+            char* p = base + (size_t(i) * L.si + size_t(j) * L.sj + 1) * es;
             if (write) f.write(p, row);
             else f.read(p, row);
         }
@@ -46,9 +47,9 @@ void io_owned(std::fstream& f, char* base, int nx, int ny, int nz, int pitch, in
 
 }  // namespace
 
-void write_checkpoint(const std::string& dir, const CheckpointHeader& h, const void* prev,
-                      const void* cur, int nx, int ny, int nz, int pitch,
-                      const std::vector<double>& max_abs, const std::vector<double>& max_rel) {
+void write_checkpoint(const std::string& dir, const CheckpointHeader& h, const HostLevel& prev,
+                      const HostLevel& cur, const std::vector<double>& max_abs,
+                      const std::vector<double>& max_rel) {
     std::string path = checkpoint_path(dir, h.rank);
     std::string tmp = path + ".tmp";
     {
@@ -58,18 +59,27 @@ void write_checkpoint(const std::string& dir, const CheckpointHeader& h, const v
         int n = h.layer + 1;
         f.write(reinterpret_cast<const char*>(max_abs.data()), sizeof(double) * n);
         f.write(reinterpret_cast<const char*>(max_rel.data()), sizeof(double) * n);
-        io_owned(f, const_cast<char*>(static_cast<const char*>(prev)), nx, ny, nz, pitch,
-                 h.elem_size, true);
-        io_owned(f, const_cast<char*>(static_cast<const char*>(cur)), nx, ny, nz, pitch,
-                 h.elem_size, true);
+        io_owned(f, prev, h.elem_size, true);
+        io_owned(f, cur, h.elem_size, true);
         W3D_REQUIRE(f.good(), "checkpoint write failed " + tmp);
     }
     W3D_REQUIRE(std::rename(tmp.c_str(), path.c_str()) == 0, "cannot rename " + tmp);
 }
 
-int read_checkpoint_raw(const std::string& dir, const CheckpointHeader& expect, void* levels[3],
-                        int nx, int ny, int nz, int pitch, std::vector<double>& max_abs,
-                        std::vector<double>& max_rel) {
+int checkpoint_layer(const std::string& dir, int rank) {
+    std::string path = checkpoint_path(dir, rank);
+    std::fstream f(path, std::ios::in | std::ios::binary);
+    W3D_REQUIRE(f.good(), "cannot open checkpoint " + path);
+    CheckpointHeader h;
+    f.read(reinterpret_cast<char*>(&h), sizeof(h));
+    W3D_REQUIRE(f.good() && std::memcmp(h.magic, CheckpointHeader().magic, 8) == 0,
+                "not a checkpoint: " + path);
+    return h.layer;
+}
+
+int read_checkpoint(const std::string& dir, const CheckpointHeader& expect, const HostLevel& prev,
+                    const HostLevel& cur, std::vector<double>& max_abs,
+                    std::vector<double>& max_rel) {
     std::string path = checkpoint_path(dir, expect.rank);
     std::fstream f(path, std::ios::in | std::ios::binary);
     W3D_REQUIRE(f.good(), "cannot open checkpoint " + path);
@@ -90,8 +100,8 @@ int read_checkpoint_raw(const std::string& dir, const CheckpointHeader& expect, 
     max_rel.assign(n + 1, 0.0);
     f.read(reinterpret_cast<char*>(max_abs.data()), sizeof(double) * (n + 1));
     f.read(reinterpret_cast<char*>(max_rel.data()), sizeof(double) * (n + 1));
-    io_owned(f, static_cast<char*>(levels[(n + 2) % 3]), nx, ny, nz, pitch, h.elem_size, false);
-    io_owned(f, static_cast<char*>(levels[n % 3]), nx, ny, nz, pitch, h.elem_size, false);
+    io_owned(f, prev, h.elem_size, false);
+    io_owned(f, cur, h.elem_size, false);
     W3D_REQUIRE(f.good(), "truncated checkpoint " + path);
     return n;
 }

@@ -30,24 +30,22 @@ struct CheckpointHeader {
 CheckpointHeader make_header(const Config& c, const Topology& t, int layer, int elem_size);
 std::string checkpoint_path(const std::string& dir, int rank);
 
-// `prev`/`cur` are padded host arrays [nx][ny][pitch] (ghost layer 1); owned nodes only
-// are written.
-void write_checkpoint(const std::string& dir, const CheckpointHeader& h, const void* prev,
-                      const void* cur, int nx, int ny, int nz, int pitch,
-                      const std::vector<double>& max_abs, const std::vector<double>& max_rel);
+// Host view of one level: element (i,j,k) of the owned block (1..X, 1..Y, 1..Z) lives at
+// origin + (i*si + j*sj + k) elements. Only owned nodes are stored.
+struct HostLevel {
+    void* origin = nullptr;
+    int X = 0, Y = 0, Z = 0;
+    long long sj = 0, si = 0;
+};
 
-// Validates the header against `expect` (layer ignored), fills the owned nodes of
-// levels[(n+2)%3] (u^{n-1}) and levels[n%3] (u^n), returns n.
-int read_checkpoint_raw(const std::string& dir, const CheckpointHeader& expect, void* levels[3],
-                        int nx, int ny, int nz, int pitch, std::vector<double>& max_abs,
-                        std::vector<double>& max_rel);
+void write_checkpoint(const std::string& dir, const CheckpointHeader& h, const HostLevel& prev,
+                      const HostLevel& cur, const std::vector<double>& max_abs,
+                      const std::vector<double>& max_rel);
 
-template <class V>
-int read_checkpoint(const std::string& dir, const CheckpointHeader& expect, V (&g)[3], int nx,
-                    int ny, int nz, int pitch, std::vector<double>& max_abs,
-                    std::vector<double>& max_rel) {
-    void* lv[3] = {g[0].data(), g[1].data(), g[2].data()};
-    return read_checkpoint_raw(dir, expect, lv, nx, ny, nz, pitch, max_abs, max_rel);
-}
+// Validates the header against `expect` (layer ignored), fills the owned nodes of `prev`
+// (u^{n-1}) and `cur` (u^n), returns n. Call checkpoint_layer() first to learn n.
+int read_checkpoint(const std::string& dir, const CheckpointHeader& expect, const HostLevel& prev,
+                    const HostLevel& cur, std::vector<double>& max_abs, std::vector<double>& max_rel);
+int checkpoint_layer(const std::string& dir, int rank);
 
 }  // namespace wave3d

@@ -434,17 +434,29 @@ private:
         }
         for (auto& R : ranks_) {
             CheckpointHeader h = make_header(cfg_, R.topo, n, sizeof(T));
-            write_checkpoint(cfg_.checkpoint_dir, h, R.g[(n + 2) % 3].data(), R.g[n % 3].data(),
-                             R.nx, R.ny, R.nz, R.nz, a, r);
+            write_checkpoint(cfg_.checkpoint_dir, h, host_level(R, (n + 2) % 3),
+                             host_level(R, n % 3), a, r);
         }
+    }
+
+    static HostLevel host_level(RankState<T>& R, int level) {
+        HostLevel L;
+        L.origin = R.g[level].data();
+        L.X = R.topo.X();
+        L.Y = R.topo.Y();
+        L.Z = R.topo.Z();
+        L.sj = R.sj;
+        L.si = R.si;
+        return L;
     }
 
     int load_checkpoints() {
         int n = -1;
         for (auto& R : ranks_) {
             CheckpointHeader h = make_header(cfg_, R.topo, 0, sizeof(T));
-            int got = read_checkpoint(cfg_.resume_dir, h, R.g, R.nx, R.ny, R.nz, R.nz, ckpt_abs_,
-                                      ckpt_rel_);
+            const int lay = checkpoint_layer(cfg_.resume_dir, R.topo.rank);
+            int got = read_checkpoint(cfg_.resume_dir, h, host_level(R, (lay + 2) % 3),
+                                      host_level(R, lay % 3), ckpt_abs_, ckpt_rel_);
             W3D_REQUIRE(n < 0 || got == n, "checkpoint layers differ between ranks");
             n = got;
         }

@@ -1,0 +1,119 @@
+// Device-side helpers shared by the stencil kernels (hip_kernels.hip, hip_tb.hip).
+// Internal to the HIP translation units (anonymous namespace per includer).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include "hip_kernels.hpp"
+#include "stencil_math.hpp"
+
+#define HIP_OK(x)                                                                      \
+    do {                                                                               \
+        hipError_t e_ = (x);                                                           \
+        if (e_ != hipSuccess)                                                          \
+            throw ::wave3d::Error(std::string("HIP error ") + hipGetErrorString(e_) + \
+                                  " at " __FILE__ ":" + std::to_string(__LINE__));     \
+    } while (0)
+
+namespace wave3d {
+namespace {
+
+constexpr int kThreads = 256;
+constexpr int kWaves = kThreads / 64;
+constexpr int kTK = 64;                  // tile columns (k) = one wave64
+constexpr int kLW = kTK + 2;             // LDS row incl. k halos
+constexpr int kNaiveTJ = kWaves;         // naive kernel: one row per wave
+
+struct BoxLaunch {
+    int i0, i1, j0, j1, k0, k1;
+    int kbase;     // k of lane 0 of the first tile (aligned to 1 + 64t)
+    int tiles_k, tiles_j, chunk;
+    int block_begin;
+};
+
+__device__ __forceinline__ u64 enc_key(double d) {
+    u64 b = (u64)__double_as_longlong(d);
+    return (b >> 63) ? ~b : (b | 0x8000000000000000ull);
+}
+
+template <class T>
+__device__ __forceinline__ T wave_max(T v) {
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+        T o = __shfl_xor(v, off, 64);
+        v = o > v ? o : v;
+    }
+    return v;
+}
+
+// Workgroup reduction of the running maxima + one atomic per slot (race-free, no
+// divergent barrier: every thread reaches the __syncthreads, cf. Appendix B5).
+template <class T>
+__device__ __forceinline__ void commit_errors(T ma, T mr, bool bad, u64* err) {
+    __shared__ double red[2][kWaves];
+    __shared__ int redb[kWaves];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    ma = wave_max(ma);
+    mr = wave_max(mr);
+    unsigned long long any = __ballot(bad);
+    if (lane == 0) {
+        red[0][w] = double(ma);
+        red[1][w] = double(mr);
+        redb[w] = any != 0ull;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double a = red[0][0], r = red[1][0];
+        int b = redb[0];
+#pragma unroll
+        for (int q = 1; q < kWaves; ++q) {
+            if (red[0][q] > a) a = red[0][q];
+            if (red[1][q] > r) r = red[1][q];
+            b |= redb[q];
+        }
+        atomicMax(err + 0, enc_key(a));
+        atomicMax(err + 1, enc_key(r));
+        if (b) atomicMax(err + 2, 1ull);
+    }
+}
+
+template <class P>
+__device__ __forceinline__ int find_box(const P& p, int bid) {
+    int b = 0;
+#pragma unroll
+    for (int q = 1; q < kMaxBoxes; ++q)
+        if (q < p.nbox && bid >= p.box[q].block_begin) b = q;
+    return b;
+}
+
+inline int cdiv(int a, int b) { return (a + b - 1) / b; }
+
+// ---- buffer addressing (T8): wave-uniform plane descriptor + 32-bit lane byte offset -----
+// An offset >= the descriptor's byte size is out of range: loads return 0, stores are
+// dropped — masked lanes use kOOB instead of a branch around the access.
+constexpr unsigned kOOB = 0x80000000u;
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t plane_rsrc(const void* base, unsigned bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, int(bytes),
+                                             0x00020000);
+}
+__device__ __forceinline__ double bload(double*, __amdgpu_buffer_rsrc_t r, unsigned off) {
+    return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0));
+}
+__device__ __forceinline__ float bload(float*, __amdgpu_buffer_rsrc_t r, unsigned off) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0));
+}
+template <class T>
+__device__ __forceinline__ T bld(__amdgpu_buffer_rsrc_t r, unsigned off) {
+    return bload((T*)nullptr, r, off);
+}
+__device__ __forceinline__ void bst(double v, __amdgpu_buffer_rsrc_t r, unsigned off) {
+    using V2 = decltype(__builtin_amdgcn_raw_buffer_load_b64(r, 0, 0, 0));
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(V2, v), r, off, 0, 0);
+}
+__device__ __forceinline__ void bst(float v, __amdgpu_buffer_rsrc_t r, unsigned off) {
+    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), r, off, 0, 0);
+}
+
+}  // namespace
+}  // namespace wave3d

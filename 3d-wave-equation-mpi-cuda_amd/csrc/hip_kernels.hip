@@ -23,32 +23,11 @@
 
 #include <algorithm>
 
-#include "hip_kernels.hpp"
-#include "stencil_math.hpp"
+#include "device_common.hpp"
 
-#define HIP_OK(x)                                                                      \
-    do {                                                                               \
-        hipError_t e_ = (x);                                                           \
-        if (e_ != hipSuccess)                                                          \
-            throw ::wave3d::Error(std::string("HIP error ") + hipGetErrorString(e_) + \
-                                  " at " __FILE__ ":" + std::to_string(__LINE__));     \
-    } while (0)
 
 namespace wave3d {
 namespace {
-
-constexpr int kThreads = 256;
-constexpr int kWaves = kThreads / 64;
-constexpr int kTK = 64;                  // tile columns (k) = one wave64
-constexpr int kLW = kTK + 2;             // LDS row incl. k halos
-constexpr int kNaiveTJ = kWaves;         // naive kernel: one row per wave
-
-struct BoxLaunch {
-    int i0, i1, j0, j1, k0, k1;
-    int kbase;     // k of lane 0 of the first tile (aligned to 1 + 64t)
-    int tiles_k, tiles_j, chunk;
-    int block_begin;
-};
 
 template <class T>
 struct StepParams {
@@ -61,7 +40,7 @@ struct StepParams {
     int nbox;
     BoxLaunch box[kMaxBoxes];
     int ei0, ei1;
-    int wsrc0, wdst0, wsrc1, wdst1;
+    int wsrc[kMaxWrap], wdst[kMaxWrap];
     T* zbuf0;
     T* zbuf1;
     int zk0, zk1;
@@ -74,70 +53,17 @@ struct StepParams {
     const T* tz;
     T hx2, hy2, hz2, coef, ct;
     T rx2, ry2, rz2;  // 1/h^2 (fast-math variants only)
+    T yx2, yy2, yz2;  // RN(1/h^2) in T for the correctly rounded constant division
     u64* err;
 };
-
-__device__ __forceinline__ u64 enc_key(double d) {
-    u64 b = (u64)__double_as_longlong(d);
-    return (b >> 63) ? ~b : (b | 0x8000000000000000ull);
-}
-
-template <class T>
-__device__ __forceinline__ T wave_max(T v) {
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) {
-        T o = __shfl_xor(v, off, 64);
-        v = o > v ? o : v;
-    }
-    return v;
-}
-
-// Workgroup reduction of the running maxima + one atomic per slot (race-free, no
-// divergent barrier: every thread reaches the __syncthreads, cf. Appendix B5).
-template <class T>
-__device__ __forceinline__ void commit_errors(T ma, T mr, bool bad, u64* err) {
-    __shared__ double red[2][kWaves];
-    __shared__ int redb[kWaves];
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    ma = wave_max(ma);
-    mr = wave_max(mr);
-    unsigned long long any = __ballot(bad);
-    if (lane == 0) {
-        red[0][w] = double(ma);
-        red[1][w] = double(mr);
-        redb[w] = any != 0ull;
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        double a = red[0][0], r = red[1][0];
-        int b = redb[0];
-#pragma unroll
-        for (int q = 1; q < kWaves; ++q) {
-            if (red[0][q] > a) a = red[0][q];
-            if (red[1][q] > r) r = red[1][q];
-            b |= redb[q];
-        }
-        atomicMax(err + 0, enc_key(a));
-        atomicMax(err + 1, enc_key(r));
-        if (b) atomicMax(err + 2, 1ull);
-    }
-}
-
-template <class T>
-__device__ __forceinline__ int find_box(const StepParams<T>& p, int bid) {
-    int b = 0;
-#pragma unroll
-    for (int q = 1; q < kMaxBoxes; ++q)
-        if (q < p.nbox && bid >= p.box[q].block_begin) b = q;
-    return b;
-}
 
 template <class T>
 __device__ __forceinline__ void store_point(const StepParams<T>& p, int i, int j, int k, i64 o,
                                             int rowoff, T v) {
     p.u[o] = v;
-    if (i == p.wsrc0) p.u[i64(p.wdst0) * p.si + rowoff] = v;
-    if (i == p.wsrc1) p.u[i64(p.wdst1) * p.si + rowoff] = v;
+#pragma unroll
+    for (int q = 0; q < kMaxWrap; ++q)
+        if (i == p.wsrc[q]) p.u[i64(p.wdst[q]) * p.si + rowoff] = v;
     if (k == p.zk0) p.zbuf0[i64(i - 1) * p.zrow + j] = v;
     if (k == p.zk1) p.zbuf1[i64(i - 1) * p.zrow + j] = v;
     if (j == p.yj0) p.ybuf0[i64(i - 1) * p.yrow + k] = v;
@@ -265,7 +191,8 @@ __global__ void __launch_bounds__(kThreads) k_march(const StepParams<T> p) {
                 v = FIRST ? __builtin_fma(p.coef, lap, Cv[r])
                           : __builtin_fma(p.coef, lap, T(2) * Cv[r] - U2c[r]);
             } else {
-                const T lap = laplace7(Cv[r], Pv[r], Nv[r], jm, jp, km, kp, p.hx2, p.hy2, p.hz2);
+                const T lap = laplace7_cr(Cv[r], Pv[r], Nv[r], jm, jp, km, kp, p.hx2, p.hy2, p.hz2,
+                                          p.yx2, p.yy2, p.yz2);
                 v = FIRST ? taylor_first(Cv[r], lap, p.coef) : leapfrog(Cv[r], U2c[r], lap, p.coef);
             }
             if (valid[r]) {
@@ -317,8 +244,9 @@ __global__ void __launch_bounds__(kThreads) k_naive(const StepParams<T> p) {
         for (int i = ib; i <= ie; ++i) {
             const i64 o = i64(i) * si + rowoff;
             const T c = p.u1[o];
-            const T lap = laplace7(c, p.u1[o - si], p.u1[o + si], p.u1[o - p.sj],
-                                   p.u1[o + p.sj], p.u1[o - 1], p.u1[o + 1], p.hx2, p.hy2, p.hz2);
+            const T lap = laplace7_cr(c, p.u1[o - si], p.u1[o + si], p.u1[o - p.sj],
+                                      p.u1[o + p.sj], p.u1[o - 1], p.u1[o + 1], p.hx2, p.hy2,
+                                      p.hz2, p.yx2, p.yy2, p.yz2);
             const T v = FIRST ? taylor_first(c, lap, p.coef) : leapfrog(c, p.u2[o], lap, p.coef);
             store_point(p, i, j, k, o, rowoff, v);
             bad |= nonfinite(v);
@@ -333,9 +261,8 @@ __global__ void __launch_bounds__(kThreads) k_naive(const StepParams<T> p) {
 // Layer 0 (initial condition): one workgroup per 4 x 64 (j,k) tile and `chunk` planes.
 template <class T>
 __global__ void __launch_bounds__(kThreads) k_init(T* u, i64 si, int sj, Box bx, int chunk,
-                                                   int ws0, int wd0, int ws1, int wd1,
-                                                   const T* tx, const T* ty, const T* tz, T ct,
-                                                   u64* err) {
+                                                   Wrap wrap, const T* tx, const T* ty,
+                                                   const T* tz, T ct, u64* err) {
     const int k = bx.k0 + blockIdx.x * 64 + (threadIdx.x & 63);
     const int j = bx.j0 + blockIdx.y * kWaves + (threadIdx.x >> 6);
     const int ib = bx.i0 + blockIdx.z * chunk;
@@ -348,8 +275,9 @@ __global__ void __launch_bounds__(kThreads) k_init(T* u, i64 si, int sj, Box bx,
         for (int i = ib; i <= ie; ++i) {
             const T f = analytic(tx[i], tyj, tzk, ct);
             u[i64(i) * si + rowoff] = f;
-            if (i == ws0) u[i64(wd0) * si + rowoff] = f;
-            if (i == ws1) u[i64(wd1) * si + rowoff] = f;
+#pragma unroll
+            for (int q = 0; q < kMaxWrap; ++q)
+                if (i == wrap.src[q]) u[i64(wrap.dst[q]) * si + rowoff] = f;
             bad |= nonfinite(f);
             accumulate_error(f, analytic(tx[i], tyj, tzk, ct), ma, mr);
         }
@@ -358,8 +286,8 @@ __global__ void __launch_bounds__(kThreads) k_init(T* u, i64 si, int sj, Box bx,
 }
 
 template <class T>
-__global__ void k_zero_faces(T* u, i64 si, int sj, int X, int Y, int Z, int mask) {
-    const int i = 1 + blockIdx.y;
+__global__ void k_zero_faces(T* u, i64 si, int sj, int X, int Y, int Z, int G, int mask) {
+    const int i = 1 - G + blockIdx.y;  // ghost planes too: redundant ring computations read them
     const int t = 1 + blockIdx.x * blockDim.x + threadIdx.x;
     T* pl = u + i64(i) * si;
     if (t <= Y) {
@@ -402,8 +330,6 @@ __global__ void k_encode(const double* v, u64* k, int n) {
     const int t = blockIdx.x * blockDim.x + threadIdx.x;
     if (t < n) k[t] = enc_key(v[t]);
 }
-
-inline int cdiv(int a, int b) { return (a + b - 1) / b; }
 
 }  // namespace
 
@@ -461,14 +387,11 @@ void launch_step(const KernelVariant& kind, bool first, const T* u1, const T* u2
     p.u = u;
     p.si = gv.si;
     p.sj = gv.sj;
-    p.jmax = gv.ny - 1;
-    p.kmax = gv.nz - 1;
+    p.jmax = gv.jmax();
+    p.kmax = gv.kmax();
     p.ei0 = ei0;
     p.ei1 = ei1;
-    p.wsrc0 = wrap.src[0];
-    p.wdst0 = wrap.dst[0];
-    p.wsrc1 = wrap.src[1];
-    p.wdst1 = wrap.dst[1];
+    for (int q = 0; q < kMaxWrap; ++q) p.wsrc[q] = wrap.src[q], p.wdst[q] = wrap.dst[q];
     p.zbuf0 = pack.zbuf[0];
     p.zbuf1 = pack.zbuf[1];
     p.zk0 = pack.zbuf[0] ? pack.zk[0] : -7;
@@ -477,8 +400,8 @@ void launch_step(const KernelVariant& kind, bool first, const T* u1, const T* u2
     p.ybuf1 = pack.ybuf[1];
     p.yj0 = pack.ybuf[0] ? pack.yj[0] : -7;
     p.yj1 = pack.ybuf[1] ? pack.yj[1] : -7;
-    p.zrow = gv.ny;
-    p.yrow = gv.nz;
+    p.zrow = gv.Y + 2;
+    p.yrow = gv.Z + 2;
     p.tx = tx;
     p.ty = ty;
     p.tz = tz;
@@ -490,6 +413,9 @@ void launch_step(const KernelVariant& kind, bool first, const T* u1, const T* u2
     p.rx2 = T(1.0 / c.hx2);
     p.ry2 = T(1.0 / c.hy2);
     p.rz2 = T(1.0 / c.hz2);
+    p.yx2 = T(1) / T(c.hx2);
+    p.yy2 = T(1) / T(c.hy2);
+    p.yz2 = T(1) / T(c.hz2);
     p.err = err;
     const bool march = kind.march;
     const int tj_rows = march ? kWaves * kind.rows : kNaiveTJ;
@@ -497,8 +423,8 @@ void launch_step(const KernelVariant& kind, bool first, const T* u1, const T* u2
     for (int q = 0; q < nbox; ++q) {
         const Box& bx = boxes[q];
         if (bx.empty()) continue;
-        W3D_REQUIRE(bx.i0 >= 1 && bx.i1 <= gv.nx - 2 && bx.j0 >= 1 && bx.j1 <= gv.ny - 2 &&
-                        bx.k0 >= 1 && bx.k1 <= gv.nz - 2,
+        W3D_REQUIRE(bx.i0 >= 1 && bx.i1 <= gv.X && bx.j0 >= 1 && bx.j1 <= gv.Y && bx.k0 >= 1 &&
+                        bx.k1 <= gv.Z,
                     "step box outside the owned region");
         BoxLaunch& L = p.box[nb];
         L.i0 = bx.i0, L.i1 = bx.i1, L.j0 = bx.j0, L.j1 = bx.j1, L.k0 = bx.k0, L.k1 = bx.k1;
@@ -535,23 +461,23 @@ template <class T>
 void launch_init(T* u, const GridView& gv, const Box& bx, const Wrap& wrap, const T* tx,
                  const T* ty, const T* tz, double ct0, u64* err, hipStream_t s) {
     if (bx.empty()) return;
-    W3D_REQUIRE(bx.i0 >= 1 && bx.i1 <= gv.nx - 2 && bx.j1 <= gv.ny - 2 && bx.k1 <= gv.nz - 2,
+    W3D_REQUIRE(bx.i0 >= 1 && bx.i1 <= gv.X && bx.j1 <= gv.Y && bx.k1 <= gv.Z,
                 "init box outside the owned region");
     const int planes = bx.i1 - bx.i0 + 1;
     const int tiles = cdiv(bx.k1 - bx.k0 + 1, 64) * cdiv(bx.j1 - bx.j0 + 1, kWaves);
     const int chunk = std::min(planes, std::max(1, cdiv(planes * tiles, 4096 * 4)));
     dim3 grid(cdiv(bx.k1 - bx.k0 + 1, 64), cdiv(bx.j1 - bx.j0 + 1, kWaves), cdiv(planes, chunk));
-    hipLaunchKernelGGL(k_init<T>, grid, dim3(kThreads), 0, s, u, gv.si, gv.sj, bx, chunk, wrap.src[0],
-                       wrap.dst[0], wrap.src[1], wrap.dst[1], tx, ty, tz, T(ct0), err);
+    hipLaunchKernelGGL(k_init<T>, grid, dim3(kThreads), 0, s, u, gv.si, gv.sj, bx, chunk, wrap, tx,
+                       ty, tz, T(ct0), err);
     HIP_OK(hipGetLastError());
 }
 
 template <class T>
 void launch_zero_faces(T* u, const GridView& gv, int mask, hipStream_t s) {
     if (!mask) return;
-    const int X = gv.nx - 2, Y = gv.ny - 2, Z = gv.nz - 2;
-    dim3 grid(cdiv(std::max(Y, Z), 256), X);
-    hipLaunchKernelGGL(k_zero_faces<T>, grid, dim3(256), 0, s, u, gv.si, gv.sj, X, Y, Z, mask);
+    dim3 grid(cdiv(std::max(gv.Y, gv.Z), 256), gv.X + 2 * gv.G);
+    hipLaunchKernelGGL(k_zero_faces<T>, grid, dim3(256), 0, s, u, gv.si, gv.sj, gv.X, gv.Y, gv.Z,
+                       gv.G, mask);
     HIP_OK(hipGetLastError());
 }
 
@@ -562,9 +488,9 @@ void launch_faces(T* u, const GridView& gv, const FaceOp<T>* ops, int nops, bool
     if (nops <= 0) return;
     FaceOps<T> f{};
     for (int q = 0; q < nops; ++q) f.op[q] = ops[q];
-    const int len = std::max(gv.ny, gv.nz);
-    dim3 grid(cdiv(len, 256), gv.nx - 2, nops);
-    hipLaunchKernelGGL(k_faces<T>, grid, dim3(256), 0, s, u, gv.si, gv.sj, gv.ny, gv.nz, f,
+    const int len = std::max(gv.Y, gv.Z) + 2;
+    dim3 grid(cdiv(len, 256), gv.X, nops);
+    hipLaunchKernelGGL(k_faces<T>, grid, dim3(256), 0, s, u, gv.si, gv.sj, gv.Y + 2, gv.Z + 2, f,
                        to_buf);
     HIP_OK(hipGetLastError());
 }

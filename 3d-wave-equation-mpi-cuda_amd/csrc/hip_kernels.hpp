@@ -1,9 +1,10 @@
 // Host-side interface of the hand-written CDNA4 kernels (hip_kernels.hip).
 //
-// Storage of one time level (per rank): [i][j][k], k contiguous, one ghost layer.
-//   ptr(i,j,k) = g + i*si + j*sj + k,   sj = pitch (row pitch, elements), si = ny*pitch.
-// The solver offsets `g` so that (i,j,k=1) is 128-B aligned: k-tiles of 64 lanes start at
-// k = 1 + 64t and every wave row load is whole cache lines.
+// Storage of one time level (per rank): [i][j][k], k contiguous, G ghost layers per side.
+//   ptr(i,j,k) = g + i*si + j*sj + k  for logical i in [1-G, X+G] (owned 1..X), same in j,k;
+//   sj = row pitch (elements), si = (Y+2G)*sj. `g` points at logical (0,0,0) and is placed
+// so that (i,j,k=1) is 128-B aligned: 64-lane k-tiles start at k = 1 + 64t and every wave
+// row load is whole cache lines.
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -15,9 +16,13 @@
 namespace wave3d {
 
 struct GridView {
-    int nx = 0, ny = 0, nz = 0;  // padded extents (X+2, Y+2, Z+2)
-    int sj = 0;                  // row pitch (elements)
-    i64 si = 0;                  // plane stride (elements)
+    int X = 0, Y = 0, Z = 0;  // owned nodes per axis (logical indices 1..X etc.)
+    int G = 1;                // ghost depth: logical indices 1-G .. X+G exist in storage
+    int sj = 0;               // row pitch (elements)
+    i64 si = 0;               // plane stride (elements)
+    int poff = 0;             // logical (i,0,0) - physical start of plane i: j*sj+k+poff >= 0
+    int jmax() const { return Y + G; }
+    int kmax() const { return Z + G; }
 };
 
 // Up to this many boxes per launch (interior + 6 shell slabs).
@@ -39,11 +44,12 @@ struct FusedPack {
     int yj[2] = {-1, -1};
 };
 
-// Periodic self-wrap fused into the stores (dims[0] == 1): the plane `src[s]` is also
-// written to ghost plane `dst[s]`. -1 = off.
+// Periodic self-wrap fused into the stores (dims[0] == 1): plane `src[q]` is also written
+// to ghost plane `dst[q]` (depth-2 ghosts need 4 pairs). -1 = unused.
+constexpr int kMaxWrap = 4;
 struct Wrap {
-    int src[2] = {-1, -1};
-    int dst[2] = {-1, -1};
+    int src[kMaxWrap] = {-1, -1, -1, -1};
+    int dst[kMaxWrap] = {-1, -1, -1, -1};
 };
 
 // Stencil kernel variant: 2.5-D marching (rows per lane, non-temporal u^{n-2} loads) or
@@ -95,5 +101,27 @@ void launch_init_err(u64* err, int layers, hipStream_t s);
 void launch_encode_keys(const double* v, u64* k, int n, hipStream_t s);
 
 int march_rows_per_thread();
+
+// Temporal blocking: one sweep computes layers m (C) and m+1 (D) from A = u^{m-1} and
+// B = u^{m-2} (unused when m == 1), D-boxes as for launch_step. C is evaluated on a one-node
+// ring around every tile (redundantly, bitwise identical), inside `cdom` in j/k and as 0 on
+// the Dirichlet faces outside it. Needs ghost depth >= 2 of A and >= 1 of B.
+// Periodic seam: C at plane `alias.next_i` takes its x+ neighbour from `alias.next`
+// (a plane base pointer) and C at `alias.prev_i` its x- neighbour from `alias.prev` —
+// the reference keeps both x=0 and x=N planes, so the ghost copy of global N-1 must see
+// x=N, not x=0, as its neighbour (csrc/hip_tb.hip).
+template <class T>
+struct SeamAlias {
+    int next_i = -1 << 30, prev_i = -1 << 30;
+    const T* next = nullptr;
+    const T* prev = nullptr;
+};
+
+template <class T>
+void launch_tb2(int rows, bool first, const T* A, const T* B, T* C, T* D, const GridView& gv,
+                const Box* boxes, int nbox, const Box& cdom, int ei0, int ei1, const Wrap& wrapC,
+                const Wrap& wrapD, const SeamAlias<T>& alias, const T* tx, const T* ty,
+                const T* tz, const StepCoefs& cC, const StepCoefs& cD, u64* errC, u64* errD,
+                int chunk, hipStream_t s);
 
 }  // namespace wave3d

@@ -41,8 +41,10 @@ struct DevRank {
     Topology topo;
     GridView gv;
     int lead = 0;
-    T* alloc[3] = {nullptr, nullptr, nullptr};
-    T* g[3] = {nullptr, nullptr, nullptr};
+    T* alloc[4] = {nullptr, nullptr, nullptr, nullptr};
+    T* g[4] = {nullptr, nullptr, nullptr, nullptr};  // logical (0,0,0) of each level
+    i64 plane_off = 0;                                 // g - (start of logical plane 0)
+    size_t elems = 0;                                  // allocation per level
     T *tx = nullptr, *ty = nullptr, *tz = nullptr;
     HaloPlan plan;
     std::vector<T*> sbuf, rbuf;  // y/z messages only (x messages live in the grid)
@@ -50,7 +52,9 @@ struct DevRank {
     Box compute, error, owned, interior;
     std::vector<Box> shell;
     int zero_mask = 0;
-    Wrap wrap;
+    Wrap wrap;                   // single-step periodic self-wrap (depth 1)
+    Wrap wrap2;                  // depth-2 self-wrap (temporal blocking: IC and D layers)
+    Box cdom;                    // temporal blocking: where C is a stencil value
     FusedPack<T> pack;           // pointers into sbuf
 };
 
@@ -68,8 +72,13 @@ public:
             world_ = std::max(1, c.ranks);
             for (int r = 0; r < world_; ++r) local_.push_back(r);
         }
-        kind_ = parse_kernel_variant(c.kernel);
+        tb_ = c.kernel == "tb2" || c.kernel == "tb2r4";
+        tb_rows_ = c.kernel == "tb2r4" ? 4 : 2;
+        kind_ = parse_kernel_variant(tb_ ? std::string("auto") : c.kernel);
         naive_.march = false;
+        G_ = tb_ ? 2 : 1;
+        L_ = tb_ ? 4 : 3;
+        W3D_REQUIRE(!tb_ || world_ == 1, "--kernel tb2: multi-rank temporal blocking not supported yet");
         // interior/shell split + comm stream whenever there is a remote halo to hide
         overlap_ = c.overlap && (ext_ != nullptr || world_ > 1);
     }
@@ -93,7 +102,7 @@ public:
         res.Np = world_;
         res.dtype = cfg_.dtype;
         res.backend = "hip";
-        res.kernel = kernel_variant_name(kind_);
+        res.kernel = tb_ ? (tb_rows_ == 4 ? "tb2r4" : "tb2") : kernel_variant_name(kind_);
         res.courant = prob_.courant;
         res.transport = ext_ ? ext_->name() : (world_ > 1 ? "loopback" : "self");
         for (int a = 0; a < 3; ++a) res.dims[a] = ranks_[0].topo.dims[a];
@@ -127,17 +136,20 @@ private:
             auto& R = ranks_[q];
             R.topo = Topology::make(prob_.N, world_, local_[q], have_dims ? cfg_.dims : nullptr);
             const int X = R.topo.X(), Y = R.topo.Y(), Z = R.topo.Z();
-            R.gv.nx = X + 2;
-            R.gv.ny = Y + 2;
-            R.gv.nz = Z + 2;
-            R.gv.sj = ((Z + 2 + A - 1) / A) * A;
-            R.gv.si = i64(R.gv.ny) * R.gv.sj;
-            R.lead = A - 1;
-            const size_t elems = size_t(R.lead) + size_t(R.gv.nx) * size_t(R.gv.si);
-            for (int l = 0; l < 3; ++l) {
-                HIP_CHECK(hipMalloc(&R.alloc[l], elems * sizeof(T)));
-                HIP_CHECK(hipMemset(R.alloc[l], 0, elems * sizeof(T)));
-                R.g[l] = R.alloc[l] + R.lead;
+            // row: k = 1-G .. Z+G at offset A-1+k (k = 1 on a 128-B boundary)
+            R.gv.X = X;
+            R.gv.Y = Y;
+            R.gv.Z = Z;
+            R.gv.G = G_;
+            R.gv.sj = ((A + Z + G_ + A - 1) / A) * A;
+            R.gv.si = i64(Y + 2 * G_) * R.gv.sj;
+            R.plane_off = i64(G_ - 1) * R.gv.sj + (A - 1);
+            R.lead = int(R.plane_off);
+            R.elems = size_t(X + 2 * G_) * size_t(R.gv.si);
+            for (int l = 0; l < L_; ++l) {
+                HIP_CHECK(hipMalloc(&R.alloc[l], R.elems * sizeof(T)));
+                HIP_CHECK(hipMemset(R.alloc[l], 0, R.elems * sizeof(T)));
+                R.g[l] = R.alloc[l] + i64(G_ - 1) * R.gv.si + R.plane_off;
             }
             auto upload = [&](const std::vector<double>& tab, int n, int off) {
                 std::vector<T> v(n + 2, T(0));
@@ -150,7 +162,7 @@ private:
             R.tx = upload(tabx, X, R.topo.off[0]);
             R.ty = upload(taby, Y, R.topo.off[1]);
             R.tz = upload(tabz, Z, R.topo.off[2]);
-            R.plan = make_halo_plan(R.topo, R.gv.si, R.gv.nz);
+            R.plan = make_halo_plan(R.topo, R.gv.si, Z + 2);
             if (R.plan.self_x) W3D_REQUIRE(X >= 3, "periodic self-wrap needs >= 3 x planes");
             R.sbuf.assign(R.plan.sends.size(), nullptr);
             R.rbuf.assign(R.plan.recvs.size(), nullptr);
@@ -173,7 +185,18 @@ private:
                 R.wrap.dst[0] = 0;
                 R.wrap.src[1] = t.x_send_minus();  // global 1   -> ghost X+1
                 R.wrap.dst[1] = X + 1;
+                // depth 2: global N-2, N-1 -> ghosts -1, 0; global 1, 2 -> ghosts X+1, X+2
+                R.wrap2.src[0] = X - 2, R.wrap2.dst[0] = -1;
+                R.wrap2.src[1] = X - 1, R.wrap2.dst[1] = 0;
+                R.wrap2.src[2] = 2, R.wrap2.dst[2] = X + 1;
+                R.wrap2.src[3] = 3, R.wrap2.dst[3] = X + 2;
+                if (tb_) W3D_REQUIRE(X >= 5, "temporal blocking self-wrap needs >= 5 x planes");
             }
+            R.cdom = R.compute;
+            if (t.nbr[1][0] >= 0) R.cdom.j0 -= 1;
+            if (t.nbr[1][1] >= 0) R.cdom.j1 += 1;
+            if (t.nbr[2][0] >= 0) R.cdom.k0 -= 1;
+            if (t.nbr[2][1] >= 0) R.cdom.k1 += 1;
             for (size_t m = 0; m < R.plan.sends.size(); ++m) {
                 const auto& f = R.plan.sends[m];
                 if (f.axis == 1) {
@@ -212,7 +235,7 @@ private:
 
     void release() {
         for (auto& R : ranks_) {
-            for (int l = 0; l < 3; ++l) (void)hipFree(R.alloc[l]);
+            for (int l = 0; l < 4; ++l) (void)hipFree(R.alloc[l]);
             (void)hipFree(R.tx);
             (void)hipFree(R.ty);
             (void)hipFree(R.tz);
@@ -230,7 +253,11 @@ private:
     }
 
     // ---- helpers ----------------------------------------------------------------------
-    T* plane(DevRank<T>& R, int level, int i) { return R.g[level] + i64(i) * R.gv.si; }
+    // start of the contiguous block of logical plane i (all rows, ghosts included)
+    T* plane(DevRank<T>& R, int level, int i) {
+        return R.g[level] + i64(i) * R.gv.si - R.plane_off;
+    }
+    int lvl(int n) const { return n % L_; }
 
     int send_plane(const DevRank<T>& R, int side) const {
         return side ? R.topo.x_send_plus() : R.topo.x_send_minus();
@@ -238,12 +265,12 @@ private:
 
     void* send_ptr(DevRank<T>& R, size_t m, int n) {
         const auto& f = R.plan.sends[m];
-        if (f.axis == 0) return plane(R, n % 3, send_plane(R, f.side));
+        if (f.axis == 0) return plane(R, lvl(n), send_plane(R, f.side));
         return R.sbuf[m];
     }
     void* recv_ptr(DevRank<T>& R, size_t m, int n) {
         const auto& f = R.plan.recvs[m];
-        if (f.axis == 0) return plane(R, n % 3, f.side ? R.topo.X() + 1 : 0);
+        if (f.axis == 0) return plane(R, lvl(n), f.side ? R.topo.X() + 1 : 0);
         return R.rbuf[m];
     }
 
@@ -259,11 +286,28 @@ private:
 
     void step_boxes(DevRank<T>& R, int n, const Box* boxes, int nbox, const KernelVariant& kind,
                     hipStream_t s) {
-        const T* u1 = R.g[(n + 2) % 3];
-        const T* u2 = R.g[(n + 1) % 3];
-        launch_step<T>(kind, n == 1, u1, u2, R.g[n % 3], R.gv, boxes, nbox, R.error.i0,
+        const T* u1 = R.g[lvl(n + L_ - 1)];
+        const T* u2 = R.g[lvl(n + L_ - 2)];
+        launch_step<T>(kind, n == 1, u1, u2, R.g[lvl(n)], R.gv, boxes, nbox, R.error.i0,
                        R.error.i1, R.wrap, R.pack, R.tx, R.ty, R.tz, coefs(n),
                        R.err + size_t(n) * kSlotsPerLayer, cfg_.chunk, s);
+    }
+
+    // temporal-blocking sweep: layers m (C) and m+1 (D) from m-1 (A) and m-2 (B)
+    void sweep(DevRank<T>& R, int m, hipStream_t s) {
+        const T* A = R.g[lvl(m + L_ - 1)];
+        const T* B = R.g[lvl(m + L_ - 2)];
+        SeamAlias<T> al;
+        if (R.plan.self_x) {
+            al.next_i = 0;  // ghost copy of N-1 sees x=N (own plane X) as its x+ neighbour
+            al.next = A + i64(R.topo.X()) * R.gv.si;
+            al.prev_i = R.topo.X() + 1;  // ghost copy of 1 sees x=0 (own plane 1) as x-
+            al.prev = A + i64(1) * R.gv.si;
+        }
+        launch_tb2<T>(tb_rows_, m == 1, A, B, R.g[lvl(m)], R.g[lvl(m + 1)], R.gv, &R.compute, 1,
+                      R.cdom, R.error.i0, R.error.i1, R.wrap, R.wrap2, al, R.tx, R.ty, R.tz,
+                      coefs(m), coefs(m + 1), R.err + size_t(m) * kSlotsPerLayer,
+                      R.err + size_t(m + 1) * kSlotsPerLayer, cfg_.chunk, s);
     }
 
     void pack_faces(DevRank<T>& R, int n, hipStream_t s, bool to_buf) {
@@ -279,18 +323,18 @@ private:
             if (to_buf) o.index = f.side ? R.topo.ext[f.axis] : 1;
             else o.index = f.side ? R.topo.ext[f.axis] + 1 : 0;
         }
-        launch_faces<T>(R.g[n % 3], R.gv, ops, k, to_buf, s);
+        launch_faces<T>(R.g[lvl(n)], R.gv, ops, k, to_buf, s);
     }
 
     void inject_after_exchange(DevRank<T>& R, int n, hipStream_t s) {
         if (fault_.kind == "drop_face" && fault_.hits(R.topo.rank, n))
-            HIP_CHECK(hipMemsetAsync(plane(R, n % 3, 0), 0, R.gv.si * sizeof(T), s));
+            HIP_CHECK(hipMemsetAsync(plane(R, lvl(n), 0), 0, R.gv.si * sizeof(T), s));
     }
     void inject_after_compute(DevRank<T>& R, int n, hipStream_t s) {
         if (fault_.kind == "nan" && fault_.hits(R.topo.rank, n)) {
             const Box& b = R.compute;
             if (b.empty()) return;
-            T* p = R.g[n % 3] + i64((b.i0 + b.i1) / 2) * R.gv.si + i64((b.j0 + b.j1) / 2) * R.gv.sj +
+            T* p = R.g[lvl(n)] + i64((b.i0 + b.i1) / 2) * R.gv.si + i64((b.j0 + b.j1) / 2) * R.gv.sj +
                    (b.k0 + b.k1) / 2;
             HIP_CHECK(hipMemsetAsync(p, 0xFF, sizeof(T), s));
         }
@@ -367,8 +411,8 @@ private:
         } else {
             prof_mark(s_comp_, 0);
             for (auto& R : ranks_) {
-                launch_init<T>(R.g[0], R.gv, R.owned, R.wrap, R.tx, R.ty, R.tz, ct_[0], R.err,
-                               s_comp_);
+                launch_init<T>(R.g[0], R.gv, R.owned, tb_ ? R.wrap2 : R.wrap, R.tx, R.ty, R.tz,
+                               ct_[0], R.err, s_comp_);
                 pack_faces(R, 0, s_comp_, true);
             }
             prof_mark(s_comp_, 1);
@@ -376,11 +420,17 @@ private:
         }
         res.aborted = false;
         int done = start - 1;
-        for (int n = start; n <= K; ++n) {
+        for (int n = start; n <= K;) {
+            // temporal blocking: layers n and n+1 in one sweep; a lone last layer single-step
+            const int span = (tb_ && n + 1 <= K) ? 2 : 1;
             prof_mark(s_comp_, 0);
-            for (auto& R : ranks_)
-                if (n <= 3 || n == start) launch_zero_faces<T>(R.g[n % 3], R.gv, R.zero_mask, s_comp_);
-            if (overlap_) {
+            for (int q = n; q < n + span; ++q)
+                for (auto& R : ranks_)
+                    if (q <= L_ || q == start)
+                        launch_zero_faces<T>(R.g[lvl(q)], R.gv, R.zero_mask, s_comp_);
+            if (span == 2) {
+                for (auto& R : ranks_) sweep(R, n, s_comp_);
+            } else if (overlap_) {
                 for (auto& R : ranks_)
                     if (!R.interior.empty()) step_boxes(R, n, &R.interior, 1, kind_, s_comp_);
                 HIP_CHECK(hipStreamWaitEvent(s_comp_, ev_halo_, 0));
@@ -391,15 +441,21 @@ private:
             } else {
                 for (auto& R : ranks_) step_boxes(R, n, &R.compute, 1, kind_, s_comp_);
             }
-            for (auto& R : ranks_) inject_after_compute(R, n, s_comp_);
+            for (int q = n; q < n + span; ++q)
+                for (auto& R : ranks_) inject_after_compute(R, q, s_comp_);
             prof_mark(s_comp_, 1);
-            if (n < K) issue_exchange(n);
-            done = n;
-            if (cfg_.checkpoint_every > 0 && n % cfg_.checkpoint_every == 0 && n < K)
-                save_checkpoints(n);
-            if (cfg_.check_every > 0 && (n % cfg_.check_every == 0 || n == K)) {
-                if (check_layer(n, res)) break;
+            const int last = n + span - 1;
+            if (last < K) issue_exchange(last);
+            done = last;
+            bool ck = false, stop = false;
+            for (int q = n; q <= last; ++q) {
+                ck |= cfg_.checkpoint_every > 0 && q % cfg_.checkpoint_every == 0;
+                if (cfg_.check_every > 0 && (q % cfg_.check_every == 0 || q == K) && !stop)
+                    stop = check_layer(q, res);
             }
+            if (stop) break;
+            if (ck && last < K) save_checkpoints(last);
+            n += span;
         }
         res.layers_done = done;
 
@@ -524,49 +580,63 @@ private:
         return a;
     }
 
+    HostLevel host_level(DevRank<T>& R, std::vector<T>& h, int level) {
+        HostLevel L;
+        L.origin = h.data() + (R.g[level] - R.alloc[level]);
+        L.X = R.topo.X();
+        L.Y = R.topo.Y();
+        L.Z = R.topo.Z();
+        L.sj = R.gv.sj;
+        L.si = R.gv.si;
+        return L;
+    }
+
     void save_checkpoints(int n) {
         std::vector<double> ar = global_errors_upto(n);
         std::vector<double> a(ar.begin(), ar.begin() + prob_.K + 1), r(ar.begin() + prob_.K + 1, ar.end());
         HIP_CHECK(hipDeviceSynchronize());
         for (auto& R : ranks_) {
-            const size_t elems = size_t(R.gv.nx) * R.gv.si;
-            std::vector<T> prev(elems), cur(elems);
-            HIP_CHECK(hipMemcpy(prev.data(), R.g[(n + 2) % 3], elems * sizeof(T), hipMemcpyDeviceToHost));
-            HIP_CHECK(hipMemcpy(cur.data(), R.g[n % 3], elems * sizeof(T), hipMemcpyDeviceToHost));
+            const int lp = lvl(n + L_ - 1), lc = lvl(n);
+            std::vector<T> prev(R.elems), cur(R.elems);
+            HIP_CHECK(hipMemcpy(prev.data(), R.alloc[lp], R.elems * sizeof(T), hipMemcpyDeviceToHost));
+            HIP_CHECK(hipMemcpy(cur.data(), R.alloc[lc], R.elems * sizeof(T), hipMemcpyDeviceToHost));
             CheckpointHeader h = make_header(cfg_, R.topo, n, sizeof(T));
-            write_checkpoint(cfg_.checkpoint_dir, h, prev.data(), cur.data(), R.gv.nx, R.gv.ny,
-                             R.gv.nz, R.gv.sj, a, r);
+            write_checkpoint(cfg_.checkpoint_dir, h, host_level(R, prev, lp), host_level(R, cur, lc),
+                             a, r);
         }
+    }
+
+    void copy_plane(DevRank<T>& R, int level, int src, int dst) {
+        HIP_CHECK(hipMemcpy(plane(R, level, dst), plane(R, level, src), R.gv.si * sizeof(T),
+                            hipMemcpyDeviceToDevice));
     }
 
     int load_checkpoints() {
         int n = -1;
         HIP_CHECK(hipDeviceSynchronize());
         for (auto& R : ranks_) {
-            const size_t elems = size_t(R.gv.nx) * R.gv.si;
-            std::vector<T> lv[3] = {std::vector<T>(elems, T(0)), std::vector<T>(elems, T(0)),
-                                    std::vector<T>(elems, T(0))};
+            const int got_layer = checkpoint_layer(cfg_.resume_dir, R.topo.rank);
+            const int lp = lvl(got_layer + L_ - 1), lc = lvl(got_layer);
+            std::vector<T> prev(R.elems, T(0)), cur(R.elems, T(0));
             CheckpointHeader h = make_header(cfg_, R.topo, 0, sizeof(T));
-            int got = read_checkpoint(cfg_.resume_dir, h, lv, R.gv.nx, R.gv.ny, R.gv.nz, R.gv.sj,
-                                      ckpt_abs_, ckpt_rel_);
+            int got = read_checkpoint(cfg_.resume_dir, h, host_level(R, prev, lp),
+                                      host_level(R, cur, lc), ckpt_abs_, ckpt_rel_);
             W3D_REQUIRE(n < 0 || got == n, "checkpoint layers differ between ranks");
             n = got;
-            for (int l = 0; l < 3; ++l)
-                HIP_CHECK(hipMemcpy(R.g[l], lv[l].data(), elems * sizeof(T), hipMemcpyHostToDevice));
-            // self-wrap ghosts of both levels, then face packs for the remote exchange
-            for (int lvl : {n - 1, n}) {
-                if (R.plan.self_x) {
-                    HIP_CHECK(hipMemcpy(plane(R, lvl % 3, 0), plane(R, lvl % 3, R.topo.x_send_plus()),
-                                        R.gv.si * sizeof(T), hipMemcpyDeviceToDevice));
-                    HIP_CHECK(hipMemcpy(plane(R, lvl % 3, R.topo.X() + 1),
-                                        plane(R, lvl % 3, R.topo.x_send_minus()),
-                                        R.gv.si * sizeof(T), hipMemcpyDeviceToDevice));
-                }
+            HIP_CHECK(hipMemcpy(R.alloc[lp], prev.data(), R.elems * sizeof(T), hipMemcpyHostToDevice));
+            HIP_CHECK(hipMemcpy(R.alloc[lc], cur.data(), R.elems * sizeof(T), hipMemcpyHostToDevice));
+            if (R.plan.self_x) {  // periodic self-wrap ghosts of both levels
+                const Wrap& wc = tb_ ? R.wrap2 : R.wrap;  // u^n is the next A (depth 2 for tb)
+                for (int q = 0; q < kMaxWrap; ++q)
+                    if (wc.src[q] >= 1) copy_plane(R, lc, wc.src[q], wc.dst[q]);
+                for (int q = 0; q < kMaxWrap; ++q)
+                    if (R.wrap.src[q] >= 1) copy_plane(R, lp, R.wrap.src[q], R.wrap.dst[q]);
             }
         }
-        for (int lvl : {n - 1, n}) {
-            for (auto& R : ranks_) pack_faces(R, lvl, s_comp_, true);
-            exchange(lvl, s_comp_);
+        W3D_REQUIRE(!tb_ || world_ == 1, "resume with temporal blocking: single rank only");
+        for (int l : {n - 1, n}) {
+            for (auto& R : ranks_) pack_faces(R, l, s_comp_, true);
+            exchange(l, s_comp_);
         }
         HIP_CHECK(hipEventRecord(ev_halo_, s_comp_));
         return n;
@@ -577,6 +647,10 @@ private:
     Problem prob_;
     FaultSpec fault_;
     KernelVariant kind_, naive_;
+    bool tb_ = false;   // temporal blocking (2 layers per sweep)
+    int tb_rows_ = 2;
+    int G_ = 1;         // ghost depth
+    int L_ = 3;         // time levels kept
     bool overlap_ = false;
     int world_ = 1;
     std::vector<int> local_;

@@ -74,6 +74,35 @@ W3D_HD void accumulate_error(T u, T f, T& mabs, T& mrel) {
     if (er > mrel) mrel = er;
 }
 
+// ---- correctly rounded division by a constant ----------------------------------------
+// q = a*y, r = a - q*b (exact by FMA), q' = q + r*y with y = RN(1/b) is RN(a/b) absent
+// under/overflow (Markstein's theorem). Three FP ops instead of the ~10-instruction IEEE
+// division sequence, bitwise identical to a/b (checked against the reference's true
+// divisions by the CPU/GPU parity tests).
+W3D_HD double fma_t(double a, double b, double c) { return __builtin_fma(a, b, c); }
+W3D_HD float fma_t(float a, float b, float c) { return __builtin_fmaf(a, b, c); }
+
+template <class T>
+W3D_HD T div_const(T a, T b, T y) {
+    T q = a * y;
+    T r = fma_t(-q, b, a);
+    return fma_t(r, y, q);
+}
+
+template <class T>
+W3D_HD T laplace7_cr(T c, T xm, T xp, T ym, T yp, T zm, T zp, T hx2, T hy2, T hz2, T rx2, T ry2,
+                     T rz2) {
+#ifdef __clang__
+#pragma clang fp contract(off)
+#endif
+    T two_c = T(2) * c;
+    T ans = T(0);
+    ans += div_const(xm - two_c + xp, hx2, rx2);
+    ans += div_const(ym - two_c + yp, hy2, ry2);
+    ans += div_const(zm - two_c + zp, hz2, rz2);
+    return ans;
+}
+
 // ---- fast-math variants (not bitwise-reproducible: reciprocal multiplies, FMAs) --------
 template <class T>
 W3D_HD T laplace7_fast(T c, T xm, T xp, T ym, T yp, T zm, T zp, T rx2, T ry2, T rz2) {

@@ -21,7 +21,7 @@ def _fmt(r):
     return [(fmt6(a), fmt6(b)) for a, b in zip(r.max_abs, r.max_rel)]
 
 
-@pytest.mark.parametrize("kernel", ["march", "naive", "auto", "march8"])
+@pytest.mark.parametrize("kernel", ["march", "naive", "auto", "march8", "tb2", "tb2r4"])
 def test_golden_n32(C, kernel):
     import wave3d
     from wave3d.utils import GOLDEN_N32_K20
@@ -129,3 +129,35 @@ def test_session_reuse(C):
     r1 = sess.solve(args)
     r2 = sess.solve(args)
     assert r1["max_abs"] == r2["max_abs"]
+
+
+@pytest.mark.parametrize("kernel", ["tb2", "tb2r4"])
+@pytest.mark.parametrize("N,K,L,ic", [(37, 12, (1.7, 2.2, "pi"), "shifted"),
+                                      (30, 13, ("pi", "pi", "pi"), "shifted"),
+                                      (21, 1, (1.0, 1.3, 0.9), "ref"),
+                                      (70, 9, ("pi", 1.5, "pi"), "ref"),
+                                      (12, 6, ("pi", "pi", "pi"), "shifted")])
+def test_temporal_blocking_bitwise(C, kernel, N, K, L, ic):
+    """Two layers per sweep (redundant ring evaluation, periodic seam alias) must reproduce the
+    OpenMP oracle bit for bit, for even and odd K."""
+    import wave3d
+
+    p = wave3d.WaveProblem(N, Lx=L[0], Ly=L[1], Lz=L[2], timesteps=K, ic=ic)
+    g = _solve(p, kernel=kernel)
+    c = _solve(p, backend="cpu", threads=4)
+    assert g.kernel == kernel
+    assert g.max_abs == c.max_abs and g.max_rel == c.max_rel
+
+
+def test_temporal_blocking_fp32_and_resume(C, tmp_path):
+    import wave3d
+
+    p32 = wave3d.WaveProblem(48, timesteps=20, dtype="fp32")
+    a, b = _solve(p32), _solve(p32, kernel="tb2")
+    assert b.max_abs[-1] == pytest.approx(a.max_abs[-1], rel=1e-3)
+    p = wave3d.WaveProblem(26, timesteps=14, ic="shifted")
+    full = _solve(p, kernel="tb2")
+    _solve(p, kernel="tb2", checkpoint_every=6, checkpoint_dir=str(tmp_path))
+    res = _solve(p, kernel="tb2", resume=str(tmp_path))
+    assert res.extra["resumed_from"] == 12
+    assert res.max_abs == full.max_abs and res.max_rel == full.max_rel
