@@ -56,7 +56,20 @@ struct DevRank {
     Wrap wrap2;                  // depth-2 self-wrap (temporal blocking: IC and D layers)
     Box cdom;                    // temporal blocking: where C is a stencil value
     FusedPack<T> pack;           // pointers into sbuf
+    // temporal blocking across ranks (x slabs): plane messages, seam alias plane, boxes
+    struct PlaneMsg {
+        int peer, tag;
+        int level;      // 0 = A level (D of the sweep), 1 = B level (C of the sweep)
+        int plane;      // first logical plane; kAliasPlane = the alias buffer
+        int nplanes;
+    };
+    std::vector<PlaneMsg> tb_sends, tb_recvs;
+    T* alias_buf = nullptr;      // one plane: x=N (first x-rank) or x=0 (last x-rank)
+    Box tb_interior;
+    std::vector<Box> tb_shell;
 };
+
+constexpr int kAliasPlane = -1000;
 
 template <class T>
 class HipSolver {
@@ -72,13 +85,22 @@ public:
             world_ = std::max(1, c.ranks);
             for (int r = 0; r < world_; ++r) local_.push_back(r);
         }
-        tb_ = c.kernel == "tb2" || c.kernel == "tb2r4";
-        tb_rows_ = c.kernel == "tb2r4" ? 4 : 2;
+        // "auto": temporal blocking (tb2r4, measured fastest on MI355X, profiles/) whenever the
+        // decomposition allows it (one rank, or x slabs); otherwise the single-step march2.
+        const bool yz_split = (c.dims[1] > 1 || c.dims[2] > 1);
+        const bool auto_tb = c.kernel == "auto" && !yz_split;
+        tb_ = auto_tb || c.kernel == "tb2" || c.kernel == "tb2r4" || c.kernel == "tb2r8";
+        tb_rows_ = (auto_tb || c.kernel == "tb2r4") ? 4 : (c.kernel == "tb2r8" ? 8 : 2);
+        if (tb_ && cfg_.chunk == 0) cfg_.chunk = 48;
         kind_ = parse_kernel_variant(tb_ ? std::string("auto") : c.kernel);
         naive_.march = false;
         G_ = tb_ ? 2 : 1;
         L_ = tb_ ? 4 : 3;
-        W3D_REQUIRE(!tb_ || world_ == 1, "--kernel tb2: multi-rank temporal blocking not supported yet");
+        // temporal blocking across ranks: 2-deep x halos, so the decomposition is x slabs
+        if (tb_ && world_ > 1 && !(c.dims[0] || c.dims[1] || c.dims[2])) {
+            cfg_.dims[0] = world_;
+            cfg_.dims[1] = cfg_.dims[2] = 1;
+        }
         // interior/shell split + comm stream whenever there is a remote halo to hide
         overlap_ = c.overlap && (ext_ != nullptr || world_ > 1);
     }
@@ -102,7 +124,8 @@ public:
         res.Np = world_;
         res.dtype = cfg_.dtype;
         res.backend = "hip";
-        res.kernel = tb_ ? (tb_rows_ == 4 ? "tb2r4" : "tb2") : kernel_variant_name(kind_);
+        res.kernel = tb_ ? (tb_rows_ == 2 ? std::string("tb2") : "tb2r" + std::to_string(tb_rows_))
+                         : kernel_variant_name(kind_);
         res.courant = prob_.courant;
         res.transport = ext_ ? ext_->name() : (world_ > 1 ? "loopback" : "self");
         for (int a = 0; a < 3; ++a) res.dims[a] = ranks_[0].topo.dims[a];
@@ -215,6 +238,7 @@ private:
             if (t.nbr[2][0] >= 0) in.k0 = std::max(in.k0, 2);
             if (t.nbr[2][1] >= 0) in.k1 = std::min(in.k1, Z - 1);
             R.interior = in;
+            build_tb_plan(R);
             R.shell.clear();
             auto add = [&](Box b) {
                 if (!b.empty()) R.shell.push_back(b);
@@ -242,6 +266,7 @@ private:
             for (auto* p : R.sbuf) (void)hipFree(p);
             for (auto* p : R.rbuf) (void)hipFree(p);
             (void)hipFree(R.err);
+            (void)hipFree(R.alias_buf);
         }
         ranks_.clear();
         if (s_comp_) (void)hipStreamDestroy(s_comp_);
@@ -293,8 +318,96 @@ private:
                        R.err + size_t(n) * kSlotsPerLayer, cfg_.chunk, s);
     }
 
+    // Halo plan of the temporal-blocking path (x slabs; y/z must be Dirichlet):
+    //  up:   D planes (last ? X-2 : X-1)..+1 -> peer ghosts -1..0, [last: D plane X -> peer
+    //        alias], C plane x_send_plus -> peer B-ghost 0
+    //  down: D planes (first ? 2 : 1)..+1  -> peer ghosts X+1..X+2, [first: D plane 1 -> peer
+    //        alias], C plane x_send_minus -> peer B-ghost X+1
+    // Sends are listed up then down, receives from-down then from-up: per-peer FIFO order
+    // matches on both ends also when up == down (dims[0] == 2).
+    void build_tb_plan(DevRank<T>& R) {
+        R.tb_sends.clear();
+        R.tb_recvs.clear();
+        const auto& t = R.topo;
+        const int X = t.X();
+        R.tb_interior = R.compute;
+        R.tb_shell.clear();
+        if (!tb_ || R.plan.self_x) return;
+        W3D_REQUIRE(t.dims[1] == 1 && t.dims[2] == 1,
+                    "temporal blocking across ranks needs an x-slab decomposition (--dims P,1,1)");
+        W3D_REQUIRE(X >= 4, "temporal blocking needs >= 4 x planes per rank");
+        const bool first = t.first(0), last = t.last(0);
+        const int up = t.nbr[0][1], dn = t.nbr[0][0];
+        using M = typename DevRank<T>::PlaneMsg;
+        R.tb_sends.push_back(M{up, 11, 0, last ? X - 2 : X - 1, 2});
+        if (last) R.tb_sends.push_back(M{up, 12, 0, X, 1});
+        R.tb_sends.push_back(M{up, 13, 1, t.x_send_plus(), 1});
+        R.tb_sends.push_back(M{dn, 21, 0, first ? 2 : 1, 2});
+        if (first) R.tb_sends.push_back(M{dn, 22, 0, 1, 1});
+        R.tb_sends.push_back(M{dn, 23, 1, t.x_send_minus(), 1});
+        R.tb_recvs.push_back(M{dn, 11, 0, -1, 2});
+        if (first) R.tb_recvs.push_back(M{dn, 12, 0, kAliasPlane, 1});
+        R.tb_recvs.push_back(M{dn, 13, 1, 0, 1});
+        R.tb_recvs.push_back(M{up, 21, 0, X + 1, 2});
+        if (last) R.tb_recvs.push_back(M{up, 22, 0, kAliasPlane, 1});
+        R.tb_recvs.push_back(M{up, 23, 1, X + 1, 1});
+        if (first || last) {
+            HIP_CHECK(hipMalloc(&R.alias_buf, R.gv.si * sizeof(T)));
+            HIP_CHECK(hipMemset(R.alias_buf, 0, R.gv.si * sizeof(T)));
+        }
+        // D on planes 1,2 / X-1,X depends on received ghosts (through C on 0,1 / X,X+1)
+        Box in = R.compute;
+        in.i0 = std::max(in.i0, 3);
+        in.i1 = std::min(in.i1, X - 2);
+        R.tb_interior = in;
+        if (in.empty()) {
+            R.tb_shell.push_back(R.compute);
+        } else {
+            Box a = R.compute, b = R.compute;
+            a.i1 = in.i0 - 1;
+            b.i0 = in.i1 + 1;
+            if (!a.empty()) R.tb_shell.push_back(a);
+            if (!b.empty()) R.tb_shell.push_back(b);
+        }
+    }
+
+    void* tb_ptr(DevRank<T>& R, const typename DevRank<T>::PlaneMsg& m, int mD) {
+        if (m.plane == kAliasPlane) return R.alias_buf;
+        return plane(R, lvl(m.level == 0 ? mD : mD - 1 + L_), m.plane);
+    }
+
+    // exchange after a sweep whose D layer is mD (A level = mD, B level = mD-1)
+    void exchange_tb(int mD, hipStream_t s) {
+        if (ext_) {
+            auto& R = ranks_[0];
+            std::vector<Message> snd, rcv;
+            for (auto& m : R.tb_sends)
+                snd.push_back({m.peer, m.tag, tb_ptr(R, m, mD), size_t(m.nplanes) * R.gv.si * sizeof(T)});
+            for (auto& m : R.tb_recvs)
+                rcv.push_back({m.peer, m.tag, tb_ptr(R, m, mD), size_t(m.nplanes) * R.gv.si * sizeof(T)});
+            ext_->exchange(snd, rcv, s);
+        } else {
+            for (auto& S : ranks_)
+                for (auto& m : S.tb_sends) {
+                    auto& D = ranks_[m.peer];
+                    bool done = false;
+                    for (auto& g : D.tb_recvs)
+                        if (g.peer == S.topo.rank && g.tag == m.tag) {
+                            W3D_REQUIRE(g.nplanes == m.nplanes, "tb halo size mismatch");
+                            HIP_CHECK(hipMemcpyAsync(tb_ptr(D, g, mD), tb_ptr(S, m, mD),
+                                                     size_t(m.nplanes) * S.gv.si * sizeof(T),
+                                                     hipMemcpyDeviceToDevice, s));
+                            done = true;
+                            break;
+                        }
+                    W3D_REQUIRE(done, "unmatched tb halo message");
+                }
+        }
+        for (auto& R : ranks_) inject_after_exchange(R, mD, s);
+    }
+
     // temporal-blocking sweep: layers m (C) and m+1 (D) from m-1 (A) and m-2 (B)
-    void sweep(DevRank<T>& R, int m, hipStream_t s) {
+    void sweep(DevRank<T>& R, int m, hipStream_t s, const Box* boxes = nullptr, int nbox = 0) {
         const T* A = R.g[lvl(m + L_ - 1)];
         const T* B = R.g[lvl(m + L_ - 2)];
         SeamAlias<T> al;
@@ -303,8 +416,15 @@ private:
             al.next = A + i64(R.topo.X()) * R.gv.si;
             al.prev_i = R.topo.X() + 1;  // ghost copy of 1 sees x=0 (own plane 1) as x-
             al.prev = A + i64(1) * R.gv.si;
+        } else if (R.topo.first(0)) {   // alias = x=N received from the last x-rank
+            al.next_i = 0;
+            al.next = R.alias_buf + R.plane_off;
+        } else if (R.topo.last(0)) {    // alias = x=0 received from the first x-rank
+            al.prev_i = R.topo.X() + 1;
+            al.prev = R.alias_buf + R.plane_off;
         }
-        launch_tb2<T>(tb_rows_, m == 1, A, B, R.g[lvl(m)], R.g[lvl(m + 1)], R.gv, &R.compute, 1,
+        if (!boxes) boxes = &R.compute, nbox = 1;
+        launch_tb2<T>(tb_rows_, m == 1, A, B, R.g[lvl(m)], R.g[lvl(m + 1)], R.gv, boxes, nbox,
                       R.cdom, R.error.i0, R.error.i1, R.wrap, R.wrap2, al, R.tx, R.ty, R.tz,
                       coefs(m), coefs(m + 1), R.err + size_t(m) * kSlotsPerLayer,
                       R.err + size_t(m + 1) * kSlotsPerLayer, cfg_.chunk, s);
@@ -428,7 +548,14 @@ private:
                 for (auto& R : ranks_)
                     if (q <= L_ || q == start)
                         launch_zero_faces<T>(R.g[lvl(q)], R.gv, R.zero_mask, s_comp_);
-            if (span == 2) {
+            if (span == 2 && overlap_) {
+                for (auto& R : ranks_)
+                    if (!R.tb_interior.empty()) sweep(R, n, s_comp_, &R.tb_interior, 1);
+                HIP_CHECK(hipStreamWaitEvent(s_comp_, ev_halo_, 0));
+                for (auto& R : ranks_)
+                    if (!R.tb_shell.empty())
+                        sweep(R, n, s_comp_, R.tb_shell.data(), int(R.tb_shell.size()));
+            } else if (span == 2) {
                 for (auto& R : ranks_) sweep(R, n, s_comp_);
             } else if (overlap_) {
                 for (auto& R : ranks_)
@@ -494,20 +621,26 @@ private:
     }
 
     // exchange of layer n: overlapped on the comm stream, or inline on the compute stream
+    void any_exchange(int n, hipStream_t s) {
+        if (tb_ && !ranks_[0].tb_sends.empty()) exchange_tb(n, s);  // deep x halos
+        else exchange(n, s);
+    }
+
     void issue_exchange(int n) {
         if (overlap_) {
             HIP_CHECK(hipEventRecord(ev_layer_, s_comp_));
             HIP_CHECK(hipStreamWaitEvent(s_comm_, ev_layer_, 0));
             prof_mark(s_comm_, 2);
-            exchange(n, s_comm_);
+            any_exchange(n, s_comm_);
             prof_mark(s_comm_, 3);
             HIP_CHECK(hipEventRecord(ev_halo_, s_comm_));
         } else {
             bool any = false;
-            for (auto& R : ranks_) any |= !R.plan.sends.empty() || fault_.kind == "drop_face";
+            for (auto& R : ranks_)
+                any |= !R.plan.sends.empty() || !R.tb_sends.empty() || fault_.kind == "drop_face";
             if (!any) return;
             prof_mark(s_comp_, 2);
-            exchange(n, s_comp_);
+            any_exchange(n, s_comp_);
             prof_mark(s_comp_, 3);
             HIP_CHECK(hipEventRecord(ev_halo_, s_comp_));
         }

@@ -301,7 +301,7 @@ void launch_tb2(int rows, bool first, const T* A, const T* B, T* C, T* D, const 
                 const T* tz, const StepCoefs& cC, const StepCoefs& cD, u64* errC, u64* errD,
                 int chunk, hipStream_t s) {
     W3D_REQUIRE(gv.G >= 2, "temporal blocking needs ghost depth >= 2");
-    W3D_REQUIRE(rows == 2 || rows == 4, "tb2 rows per lane must be 2 or 4");
+    W3D_REQUIRE(rows == 2 || rows == 4 || rows == 8, "tb2 rows per lane must be 2, 4 or 8");
     W3D_REQUIRE(nbox >= 1 && nbox <= kMaxBoxes, "bad box count");
     TbParams<T> p{};
     p.A = A;
@@ -368,6 +368,7 @@ void launch_tb2(int rows, bool first, const T* A, const T* B, T* C, T* D, const 
     if (nb == 0) return;
     void (*kern)(const TbParams<T>);
     if (rows == 2) kern = first ? k_tb2<T, true, 2> : k_tb2<T, false, 2>;
+    else if (rows == 8) kern = first ? k_tb2<T, true, 8> : k_tb2<T, false, 8>;
     else kern = first ? k_tb2<T, true, 4> : k_tb2<T, false, 4>;
     hipLaunchKernelGGL(kern, dim3(total), dim3(kThreads), 0, s, p);
     HIP_OK(hipGetLastError());

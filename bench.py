@@ -8,7 +8,10 @@ layer, `timesteps` leapfrog layers, the fused per-layer max-error evaluation and
 cross-rank MAX reduction. Mpoints/s = (N+1)^3 * timesteps * steps / t_wall.
 
 Scaling is weak: per-GPU work is fixed at ~513^3 nodes, the global grid grows with the GPU
-count (1 GPU: N=512 = BASELINE config 2; 8 GPUs: N=1024 on 2x2x2 = BASELINE config 4).
+count (1 GPU: N=512 = BASELINE config 2; 8 GPUs: N=1024 = BASELINE config 4's grid). The
+default kernel is temporal blocking (2 layers per sweep, 16 instead of 24 B/node/layer),
+which decomposes into x slabs with 2-deep RCCL halos; `--kernel march2` selects the
+single-step kernel on the MPI-style 3-D decomposition (2x2x2 at 8 GPUs, 6-face halos).
 Data: the analytic initial condition on a synthetic grid (the reference's own test problem).
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
@@ -40,6 +43,9 @@ def main() -> int:
     ap.add_argument("--no-overlap", action="store_true")
     ap.add_argument("--backend", default="hip", choices=["hip", "cpu"])
     ap.add_argument("--profile", action="store_true", help="per-phase timers (slower)")
+    ap.add_argument("--transport", default="rccl", choices=["rccl", "staged"],
+                    help="halo transport for N>1 (staged = rehearsal on one shared GPU)")
+    ap.add_argument("--shared-device", action="store_true", help="all ranks on device 0 (rehearsal)")
     a = ap.parse_args()
 
     import torch
@@ -61,9 +67,12 @@ def main() -> int:
 
     transport = None
     if world > 1:
-        wdist.init_from_env("nccl" if a.backend == "hip" else "gloo")
         if a.backend == "hip":
-            transport = wdist.rccl_transport(torch.cuda.current_device())
+            torch.cuda.set_device(0 if a.shared_device else local % torch.cuda.device_count())
+        nccl = a.backend == "hip" and a.transport == "rccl"
+        wdist.init_from_env("nccl" if nccl else "gloo")
+        if a.backend == "hip":
+            transport = wdist.make_transport(a.transport)
         else:
             transport = wdist.TorchHostTransport()
     elif a.backend == "hip":
@@ -95,8 +104,8 @@ def main() -> int:
     sync()
     elapsed = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64,
-                         device="cuda" if a.backend == "hip" else "cpu")
+        on_gpu = a.backend == "hip" and a.transport == "rccl"
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda" if on_gpu else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
@@ -121,7 +130,8 @@ def main() -> int:
             "model": f"wave3d leapfrog 7-point, N={N}^3, L=pi, T=1, timesteps={a.timesteps}",
             "global_batch": 1,
             "seq_len": N + 1,
-            "parallelism": f"dd{dims[0]}x{dims[1]}x{dims[2]}" + ("" if n_gpus == 1 else "-rccl"),
+            "parallelism": f"dd{dims[0]}x{dims[1]}x{dims[2]}-{res['kernel']}"
+                           + ("" if n_gpus == 1 else f"-{res['transport']}"),
             "N": N,
             "timesteps": a.timesteps,
             "kernel": res["kernel"],

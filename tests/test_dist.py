@@ -54,9 +54,19 @@ def test_cpu_gloo_matches_single_process(C, single_cpu, P):
 @pytest.mark.gpu
 @pytest.mark.parametrize("P,overlap", [(2, True), (4, True), (8, True), (2, False), (4, False)])
 def test_hip_multiprocess_shared_gpu(C, single_cpu, P, overlap):
-    extra = [] if overlap else ["--no-overlap"]
+    """Single-step kernel on the 3-D decomposition (2x2x2 at P=8), 6-face halos."""
+    extra = ["--kernel", "march2"] + ([] if overlap else ["--no-overlap"])
     r = torchrun(P, ["--backend", "hip", "--transport", "staged", "--shared-device"], ARGS + extra)
     assert r["nprocs"] == P and r["transport"] == "staged.gloo"
+    assert r["max_abs"] == single_cpu["max_abs"] and r["max_rel"] == single_cpu["max_rel"]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("P,kernel", [(2, "tb2r4"), (4, "tb2")])
+def test_hip_multiprocess_temporal_blocking(C, single_cpu, P, kernel):
+    r = torchrun(P, ["--backend", "hip", "--transport", "staged", "--shared-device"],
+                 ARGS + ["--kernel", kernel])
+    assert r["dims"] == [P, 1, 1] and r["kernel"] == kernel
     assert r["max_abs"] == single_cpu["max_abs"] and r["max_rel"] == single_cpu["max_rel"]
 
 

@@ -27,18 +27,25 @@ def test_golden_n32(C, kernel):
     from wave3d.utils import GOLDEN_N32_K20
 
     r = _solve(wave3d.WaveProblem(32, timesteps=20), kernel=kernel)
-    assert r.backend == "hip" and r.kernel == {"march": "march4", "auto": "march2"}.get(kernel, kernel)
+    assert r.backend == "hip" and r.kernel == {"march": "march4", "auto": "tb2r4"}.get(kernel, kernel)
     assert _fmt(r) == GOLDEN_N32_K20
 
 
+@pytest.mark.parametrize("kernel", ["auto", "march2", "naive"])
 @pytest.mark.parametrize("ranks,overlap", [(2, True), (2, False), (4, True), (8, True), (8, False), (3, True)])
-def test_decomposition_invariance(C, ranks, overlap):
+def test_decomposition_invariance(C, ranks, overlap, kernel):
+    """auto = temporal blocking on x slabs; march2/naive = single-step on the MPI-style 3-D
+    decomposition (2x2x2 at 8 ranks) with 6-face halos."""
     import wave3d
 
     p = wave3d.WaveProblem(40, Lx=1.3, Ly="pi", Lz=2.0, timesteps=15, ic="shifted")
-    base = _solve(p)
-    r = _solve(p, ranks=ranks, overlap=overlap)
+    base = _solve(p, kernel="march2")
+    r = _solve(p, ranks=ranks, overlap=overlap, kernel=kernel)
     assert r.transport == "loopback"
+    if kernel == "auto":
+        assert r.dims == [ranks, 1, 1]
+    elif ranks == 8:
+        assert r.dims == [2, 2, 2]
     assert r.max_abs == base.max_abs and r.max_rel == base.max_rel
 
 
@@ -161,3 +168,18 @@ def test_temporal_blocking_fp32_and_resume(C, tmp_path):
     res = _solve(p, kernel="tb2", resume=str(tmp_path))
     assert res.extra["resumed_from"] == 12
     assert res.max_abs == full.max_abs and res.max_rel == full.max_rel
+
+
+@pytest.mark.parametrize("ranks,overlap,kernel", [(2, True, "tb2"), (3, True, "tb2r4"), (4, False, "tb2"),
+                                                  (8, True, "tb2r4"), (2, False, "tb2r8")])
+def test_temporal_blocking_slabs_loopback(C, ranks, overlap, kernel):
+    """Multi-rank temporal blocking (x slabs, 2-deep halos + seam alias plane) on simulated
+    ranks, with and without the interior/shell overlap: bitwise equal to one rank."""
+    import wave3d
+
+    for K in (9, 10):
+        p = wave3d.WaveProblem(45, Lx=1.3, Ly="pi", Lz=2.0, timesteps=K, ic="shifted")
+        base = _solve(p, backend="cpu", threads=4)
+        r = _solve(p, ranks=ranks, overlap=overlap, kernel=kernel)
+        assert r.dims == [ranks, 1, 1] and r.kernel == kernel
+        assert r.max_abs == base.max_abs and r.max_rel == base.max_rel
