@@ -766,10 +766,13 @@ private:
                     if (R.wrap.src[q] >= 1) copy_plane(R, lp, R.wrap.src[q], R.wrap.dst[q]);
             }
         }
-        W3D_REQUIRE(!tb_ || world_ == 1, "resume with temporal blocking: single rank only");
-        for (int l : {n - 1, n}) {
-            for (auto& R : ranks_) pack_faces(R, l, s_comp_, true);
-            exchange(l, s_comp_);
+        if (tb_ && !ranks_[0].tb_sends.empty()) {
+            exchange_tb(n, s_comp_);  // A level = u^n (2 deep + alias), B level = u^{n-1}
+        } else {
+            for (int l : {n - 1, n}) {
+                for (auto& R : ranks_) pack_faces(R, l, s_comp_, true);
+                exchange(l, s_comp_);
+            }
         }
         HIP_CHECK(hipEventRecord(ev_halo_, s_comp_));
         return n;

@@ -88,15 +88,17 @@ def test_fp32_close(C):
     assert b.max_abs[-1] == pytest.approx(a.max_abs[-1], rel=0.05)
 
 
-def test_checkpoint_resume(C, tmp_path):
+@pytest.mark.parametrize("kernel", ["auto", "march2"])
+@pytest.mark.parametrize("K", [12, 13])
+def test_checkpoint_resume(C, tmp_path, kernel, K):
     import wave3d
 
-    p = wave3d.WaveProblem(30, timesteps=12, ic="shifted")
-    full = _solve(p, ranks=2)
+    p = wave3d.WaveProblem(30, timesteps=K, ic="shifted")
+    full = _solve(p, ranks=2, kernel=kernel)
     d = str(tmp_path)
-    _solve(p, ranks=2, checkpoint_every=5, checkpoint_dir=d)
+    _solve(p, ranks=2, checkpoint_every=5, checkpoint_dir=d, kernel=kernel)
     assert os.path.exists(os.path.join(d, "ckpt_r0.bin"))
-    res = _solve(p, ranks=2, resume=d)
+    res = _solve(p, ranks=2, resume=d, kernel=kernel)
     assert res.extra["resumed_from"] == 10
     assert res.max_abs == full.max_abs and res.max_rel == full.max_rel
 
@@ -109,7 +111,7 @@ def test_fault_detection(C):
     assert r.aborted and r.abort_layer in (4, 5)
     ok = _solve(p, check_every=1)
     assert not ok.aborted
-    bad = _solve(p, ranks=2, fault="drop_face:1:3")
+    bad = _solve(p, ranks=2, fault="drop_face:1:4")  # an exchanged layer for tb2 and march2
     assert bad.max_abs[-1] > 10 * ok.max_abs[-1]
 
 
