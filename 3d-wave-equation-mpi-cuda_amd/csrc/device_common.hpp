@@ -97,15 +97,18 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t plane_rsrc(const void* base, u
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, int(bytes),
                                              0x00020000);
 }
+// AUX = cache policy bits of the buffer instruction (0 default, 2 = nt: read-once streams)
+template <int AUX>
 __device__ __forceinline__ double bload(double*, __amdgpu_buffer_rsrc_t r, unsigned off) {
-    return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0));
+    return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, AUX));
 }
+template <int AUX>
 __device__ __forceinline__ float bload(float*, __amdgpu_buffer_rsrc_t r, unsigned off) {
-    return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0));
+    return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, AUX));
 }
-template <class T>
+template <class T, int AUX = 0>
 __device__ __forceinline__ T bld(__amdgpu_buffer_rsrc_t r, unsigned off) {
-    return bload((T*)nullptr, r, off);
+    return bload<AUX>((T*)nullptr, r, off);
 }
 __device__ __forceinline__ void bst(double v, __amdgpu_buffer_rsrc_t r, unsigned off) {
     using V2 = decltype(__builtin_amdgcn_raw_buffer_load_b64(r, 0, 0, 0));

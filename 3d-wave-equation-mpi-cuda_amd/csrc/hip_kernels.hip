@@ -36,6 +36,7 @@ struct StepParams {
     T* u;
     i64 si;
     int sj;
+    int poff;        // see GridView::poff
     int jmax, kmax;  // largest valid j / k index in storage (ny-1, nz-1)
     int nbox;
     BoxLaunch box[kMaxBoxes];
@@ -72,17 +73,13 @@ __device__ __forceinline__ void store_point(const StepParams<T>& p, int i, int j
 
 // ---------------------------------------------------------------------------------------
 // 2.5-D marching kernel (LDS tile + register-rolling i column).
-template <class T>
-__device__ __forceinline__ T ld_stream(const T* p, bool nt) {
-    return nt ? __builtin_nontemporal_load(p) : *p;
-}
-
 // R = rows (j) per lane; the workgroup tile is (4R) x 64. NT = non-temporal loads of the
 // read-once level u^{n-2}.
 template <class T, bool FIRST, int R, bool NT, bool FAST = false>
 __global__ void __launch_bounds__(kThreads) k_march(const StepParams<T> p) {
     constexpr int kRows = R;
     constexpr int kTJ = kWaves * R;
+    constexpr unsigned ES = sizeof(T);
     __shared__ T lds[2][kTJ + 2][kLW];
 
     const int bid = blockIdx.x;
@@ -105,70 +102,83 @@ __global__ void __launch_bounds__(kThreads) k_march(const StepParams<T> p) {
     const bool kload = k <= p.kmax;
     const bool kin = k >= B.k0 && k <= B.k1;
     const i64 si = p.si;
+    const unsigned pbytes = unsigned(si) * ES;
+    // byte offset of (j,k) in a plane block (kOOB = masked: loads give 0, stores dropped)
+    auto boff = [&](int j, int kk, bool ok) { return ok ? unsigned(j * p.sj + kk + p.poff) * ES : kOOB; };
+    auto prs = [&](const T* base, int i) { return plane_rsrc(base + (i64(i) * si - p.poff), pbytes); };
 
     int rowoff[kRows];
-    bool ld_ok[kRows], valid[kRows];
+    unsigned oa[kRows], ou2[kRows], os[kRows];
+    bool valid[kRows];
     T ty[kRows];
 #pragma unroll
     for (int r = 0; r < kRows; ++r) {
         const int j = jt + w * kRows + r;
         rowoff[r] = j * p.sj + k;
-        ld_ok[r] = kload && j <= p.jmax;
         valid[r] = kin && j <= B.j1;
+        oa[r] = boff(j, k, kload && j <= p.jmax);
+        ou2[r] = boff(j, k, !FIRST && valid[r]);
+        os[r] = boff(j, k, valid[r]);
         ty[r] = valid[r] ? p.ty[j] : T(0);
     }
     const T tz = kin ? p.tz[k] : T(0);
 
     // halo role of this lane: one LDS cell per plane
-    int hoff = 0, hrow = 0, hcol = 0;
+    int hrow = 0, hcol = 0;
+    unsigned hoff = kOOB;
     bool hon = false;
     if (w == 0) {  // row jt-1
-        hon = kload;
-        hoff = (jt - 1) * p.sj + k;
+        hon = true;
+        hoff = boff(jt - 1, k, kload);
         hrow = 0;
         hcol = 1 + lane;
     } else if (w == kWaves - 1) {  // row jt+TJ
         const int j = jt + kTJ;
-        hon = kload && j <= p.jmax;
-        hoff = j * p.sj + k;
+        hon = true;
+        hoff = boff(j, k, kload && j <= p.jmax);
         hrow = kTJ + 1;
         hcol = 1 + lane;
     } else if (w == 1) {  // columns kb-1 (lanes 0..TJ-1) and kb+64 (lanes 32..32+TJ-1)
         const int side = lane >> 5, rr = lane & 31;
         const int j = jt + rr;
         const int kk = side ? kb + kTK : kb - 1;
-        hon = rr < kTJ && j <= p.jmax && kk <= p.kmax;
-        hoff = j * p.sj + kk;
+        hon = rr < kTJ;
+        hoff = boff(j, kk, hon && j <= p.jmax && kk <= p.kmax);
         hrow = 1 + rr;
         hcol = side ? kTK + 1 : 0;
     }
-
-    const T* __restrict__ u1 = p.u1;
-    const T* __restrict__ u2 = p.u2;
+    constexpr int kU2Aux = NT ? 2 : 0;  // non-temporal u^{n-2} (read once)
 
     T Pv[kRows], Cv[kRows], Nv[kRows], U2c[kRows];
+    {
+        const auto r0 = prs(p.u1, ib - 1), r1 = prs(p.u1, ib), r2 = prs(p.u1, ib + 1);
+        const auto q0 = prs(p.u2, ib);
 #pragma unroll
-    for (int r = 0; r < kRows; ++r) {
-        Pv[r] = ld_ok[r] ? u1[i64(ib - 1) * si + rowoff[r]] : T(0);
-        Cv[r] = ld_ok[r] ? u1[i64(ib) * si + rowoff[r]] : T(0);
-        Nv[r] = ld_ok[r] ? u1[i64(ib + 1) * si + rowoff[r]] : T(0);
-        U2c[r] = (!FIRST && valid[r]) ? ld_stream(u2 + i64(ib) * si + rowoff[r], NT) : T(0);
+        for (int r = 0; r < kRows; ++r) {
+            Pv[r] = bld<T>(r0, oa[r]);
+            Cv[r] = bld<T>(r1, oa[r]);
+            Nv[r] = bld<T>(r2, oa[r]);
+            U2c[r] = FIRST ? T(0) : bld<T, kU2Aux>(q0, ou2[r]);
+        }
     }
-    T H = hon ? u1[i64(ib) * si + hoff] : T(0);
+    T H = bld<T>(prs(p.u1, ib), hoff);
 
     T ma = T(kErrInit), mr = T(kErrInit);
     bool bad = false;
     int buf = 0;
     for (int i = ib; i <= ie; ++i) {
         // prefetch plane i+2 (own rows), plane i+1 (halo, u2)
-        T NN[kRows], U2n[kRows], Hn = T(0);
+        T NN[kRows], U2n[kRows];
         const bool more = i < ie;
+        const auto rN = prs(p.u1, more ? i + 2 : i);
+        const auto rH = prs(p.u1, more ? i + 1 : i);
+        const auto rU = prs(p.u2, more ? i + 1 : i);
 #pragma unroll
         for (int r = 0; r < kRows; ++r) {
-            NN[r] = (more && ld_ok[r]) ? u1[i64(i + 2) * si + rowoff[r]] : T(0);
-            U2n[r] = (!FIRST && more && valid[r]) ? ld_stream(u2 + i64(i + 1) * si + rowoff[r], NT) : T(0);
+            NN[r] = bld<T>(rN, more ? oa[r] : kOOB);
+            U2n[r] = FIRST ? T(0) : bld<T, kU2Aux>(rU, more ? ou2[r] : kOOB);
         }
-        if (more && hon) Hn = u1[i64(i + 1) * si + hoff];
+        const T Hn = bld<T>(rH, more ? hoff : kOOB);
 
         // stage plane i
 #pragma unroll
@@ -178,6 +188,7 @@ __global__ void __launch_bounds__(kThreads) k_march(const StepParams<T> p) {
 
         const T sx = p.tx[i];
         const bool erow = i >= p.ei0 && i <= p.ei1;
+        T vv[kRows];
 #pragma unroll
         for (int r = 0; r < kRows; ++r) {
             const int lr = 1 + w * kRows + r;
@@ -185,26 +196,45 @@ __global__ void __launch_bounds__(kThreads) k_march(const StepParams<T> p) {
             const T jp = r == kRows - 1 ? lds[buf][lr + 1][1 + lane] : Cv[r + 1];
             const T km = lds[buf][lr][lane];
             const T kp = lds[buf][lr][lane + 2];
-            T v;
             if constexpr (FAST) {
                 const T lap = laplace7_fast(Cv[r], Pv[r], Nv[r], jm, jp, km, kp, p.rx2, p.ry2, p.rz2);
-                v = FIRST ? __builtin_fma(p.coef, lap, Cv[r])
-                          : __builtin_fma(p.coef, lap, T(2) * Cv[r] - U2c[r]);
+                vv[r] = FIRST ? __builtin_fma(p.coef, lap, Cv[r])
+                              : __builtin_fma(p.coef, lap, T(2) * Cv[r] - U2c[r]);
             } else {
                 const T lap = laplace7_cr(Cv[r], Pv[r], Nv[r], jm, jp, km, kp, p.hx2, p.hy2, p.hz2,
                                           p.yx2, p.yy2, p.yz2);
-                v = FIRST ? taylor_first(Cv[r], lap, p.coef) : leapfrog(Cv[r], U2c[r], lap, p.coef);
-            }
-            if (valid[r]) {
-                const int j = jt + w * kRows + r;
-                store_point(p, i, j, k, i64(i) * si + rowoff[r], rowoff[r], v);
-                bad |= nonfinite(v);
-                if (erow) {
-                    if constexpr (FAST) accumulate_error_fast(v, analytic(sx, ty[r], tz, p.ct), ma, mr);
-                    else accumulate_error(v, analytic(sx, ty[r], tz, p.ct), ma, mr);
-                }
+                vv[r] = FIRST ? taylor_first(Cv[r], lap, p.coef) : leapfrog(Cv[r], U2c[r], lap, p.coef);
             }
         }
+        // stores: own plane + fused periodic wrap (buffer stores, masked lanes dropped)
+        {
+            const auto rs = prs(p.u, i);
+#pragma unroll
+            for (int r = 0; r < kRows; ++r) bst(vv[r], rs, os[r]);
+#pragma unroll
+            for (int q = 0; q < kMaxWrap; ++q)
+                if (i == p.wsrc[q]) {
+                    const auto rw = prs(p.u, p.wdst[q]);
+#pragma unroll
+                    for (int r = 0; r < kRows; ++r) bst(vv[r], rw, os[r]);
+                }
+        }
+#pragma unroll
+        for (int r = 0; r < kRows; ++r) {
+            if (!valid[r]) continue;
+            const int j = jt + w * kRows + r;
+            const T v = vv[r];
+            if (k == p.zk0) p.zbuf0[i64(i - 1) * p.zrow + j] = v;
+            if (k == p.zk1) p.zbuf1[i64(i - 1) * p.zrow + j] = v;
+            if (j == p.yj0) p.ybuf0[i64(i - 1) * p.yrow + k] = v;
+            if (j == p.yj1) p.ybuf1[i64(i - 1) * p.yrow + k] = v;
+            bad |= nonfinite(v);
+            if (erow) {
+                if constexpr (FAST) accumulate_error_fast(v, analytic(sx, ty[r], tz, p.ct), ma, mr);
+                else accumulate_error(v, analytic(sx, ty[r], tz, p.ct), ma, mr);
+            }
+        }
+        (void)rowoff;
 #pragma unroll
         for (int r = 0; r < kRows; ++r) {
             Pv[r] = Cv[r];
@@ -387,6 +417,7 @@ void launch_step(const KernelVariant& kind, bool first, const T* u1, const T* u2
     p.u = u;
     p.si = gv.si;
     p.sj = gv.sj;
+    p.poff = gv.poff;
     p.jmax = gv.jmax();
     p.kmax = gv.kmax();
     p.ei0 = ei0;

@@ -112,7 +112,7 @@ int march_rows_per_thread();
 // x=N, not x=0, as its neighbour (csrc/hip_tb.hip).
 template <class T>
 struct SeamAlias {
-    int next_i = -1 << 30, prev_i = -1 << 30;
+    int next_i = -(1 << 30), prev_i = -(1 << 30);
     const T* next = nullptr;
     const T* prev = nullptr;
 };

@@ -167,6 +167,7 @@ private:
             R.gv.sj = ((A + Z + G_ + A - 1) / A) * A;
             R.gv.si = i64(Y + 2 * G_) * R.gv.sj;
             R.plane_off = i64(G_ - 1) * R.gv.sj + (A - 1);
+            R.gv.poff = int(R.plane_off);
             R.lead = int(R.plane_off);
             R.elems = size_t(X + 2 * G_) * size_t(R.gv.si);
             for (int l = 0; l < L_; ++l) {
