@@ -48,10 +48,10 @@ __device__ __forceinline__ T wave_max(T v) {
 
 // Workgroup reduction of the running maxima + one atomic per slot (race-free, no
 // divergent barrier: every thread reaches the __syncthreads, cf. Appendix B5).
-template <class T>
+template <class T, int NW = kWaves>
 __device__ __forceinline__ void commit_errors(T ma, T mr, bool bad, u64* err) {
-    __shared__ double red[2][kWaves];
-    __shared__ int redb[kWaves];
+    __shared__ double red[2][NW];
+    __shared__ int redb[NW];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     ma = wave_max(ma);
     mr = wave_max(mr);
@@ -66,7 +66,7 @@ __device__ __forceinline__ void commit_errors(T ma, T mr, bool bad, u64* err) {
         double a = red[0][0], r = red[1][0];
         int b = redb[0];
 #pragma unroll
-        for (int q = 1; q < kWaves; ++q) {
+        for (int q = 1; q < NW; ++q) {
             if (red[0][q] > a) a = red[0][q];
             if (red[1][q] > r) r = red[1][q];
             b |= redb[q];
@@ -75,6 +75,20 @@ __device__ __forceinline__ void commit_errors(T ma, T mr, bool bad, u64* err) {
         atomicMax(err + 1, enc_key(r));
         if (b) atomicMax(err + 2, 1ull);
     }
+}
+
+// XCD-aware work order. Workgroups are dispatched round-robin over the 8 XCDs
+// (blockIdx % 8), each with its own L2. Renumbering so that XCD x runs one contiguous range
+// of logical tiles keeps k- and j-neighbour tiles — which read each other's edge rows and
+// columns as halo — on the same L2 instead of always on different ones. Measured on
+// MI355X (profiles/sweep_n512_xcd_swizzle_r1.txt) it does not pay here (halo lines come
+// from the memory-side Infinity Cache either way), so it is opt-in: WAVE3D_XCD_SWIZZLE=1.
+constexpr int kXcds = 8;
+__device__ __forceinline__ int xcd_swizzle(int bid, int total, bool on) {
+    if (!on) return bid;
+    const int x = bid % kXcds, q = bid / kXcds;
+    const int base = total / kXcds, rem = total % kXcds;
+    return x * base + min(x, rem) + q;
 }
 
 template <class P>
@@ -97,6 +111,15 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t plane_rsrc(const void* base, u
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, int(bytes),
                                              0x00020000);
 }
+// Wave-uniform read of a small read-only table through the constant address space, so it
+// is a scalar load (s_load, lgkmcnt) instead of a vector load whose vmcnt wait would also
+// drain every prefetch issued before it.
+template <class T>
+__device__ __forceinline__ T ldconst(const T* base, int i) {
+    using CP = const __attribute__((address_space(4))) T*;
+    return ((CP)(base))[i];
+}
+
 // AUX = cache policy bits of the buffer instruction (0 default, 2 = nt: read-once streams)
 template <int AUX>
 __device__ __forceinline__ double bload(double*, __amdgpu_buffer_rsrc_t r, unsigned off) {

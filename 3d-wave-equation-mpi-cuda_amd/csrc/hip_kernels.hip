@@ -21,6 +21,8 @@
 // are bitwise those of mpi_new.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include <algorithm>
 
 #include "device_common.hpp"
@@ -31,6 +33,7 @@ namespace {
 
 template <class T>
 struct StepParams {
+    int xcd;  // XCD-aware tile order (xcd_swizzle)
     const T* u1;
     const T* u2;
     T* u;
@@ -82,7 +85,7 @@ __global__ void __launch_bounds__(kThreads) k_march(const StepParams<T> p) {
     constexpr unsigned ES = sizeof(T);
     __shared__ T lds[2][kTJ + 2][kLW];
 
-    const int bid = blockIdx.x;
+    const int bid = xcd_swizzle(blockIdx.x, gridDim.x, p.xcd);
     const int b = find_box(p, bid);
     const BoxLaunch B = p.box[b];
     int local = bid - B.block_begin;
@@ -253,7 +256,7 @@ __global__ void __launch_bounds__(kThreads) k_march(const StepParams<T> p) {
 // ablation (profiles/) and as a second, independent device implementation.
 template <class T, bool FIRST>
 __global__ void __launch_bounds__(kThreads) k_naive(const StepParams<T> p) {
-    const int bid = blockIdx.x;
+    const int bid = xcd_swizzle(blockIdx.x, gridDim.x, p.xcd);
     const int b = find_box(p, bid);
     const BoxLaunch B = p.box[b];
     int local = bid - B.block_begin;
@@ -365,6 +368,14 @@ __global__ void k_encode(const double* v, u64* k, int n) {
 
 int march_rows_per_thread() { return 4; }
 
+bool xcd_swizzle_enabled() {
+    static const bool on = [] {
+        const char* e = std::getenv("WAVE3D_XCD_SWIZZLE");
+        return e && e[0] == '1';
+    }();
+    return on;
+}
+
 KernelVariant parse_kernel_variant(const std::string& name) {
     KernelVariant v;
     if (name == "naive") {
@@ -412,6 +423,7 @@ void launch_step(const KernelVariant& kind, bool first, const T* u1, const T* u2
                  const StepCoefs& c, u64* err, int chunk, hipStream_t s) {
     W3D_REQUIRE(nbox >= 1 && nbox <= kMaxBoxes, "bad box count");
     StepParams<T> p{};
+    p.xcd = xcd_swizzle_enabled();
     p.u1 = u1;
     p.u2 = u2;
     p.u = u;
@@ -473,6 +485,7 @@ void launch_step(const KernelVariant& kind, bool first, const T* u1, const T* u2
                 // to balance the 256 CUs, 2 extra prologue planes per 32 computed
                 ch = std::min(32, planes);
             }
+            ch = cdiv(planes, cdiv(planes, ch));  // equal work items (no short tail chunk)
         }
         L.chunk = ch;
         L.block_begin = total;

@@ -102,6 +102,10 @@ void launch_encode_keys(const double* v, u64* k, int n, hipStream_t s);
 
 int march_rows_per_thread();
 
+// XCD-aware workgroup order for the stencil kernels (device_common.hpp xcd_swizzle);
+// opt-in via env WAVE3D_XCD_SWIZZLE=1 (ablation, not faster on MI355X).
+bool xcd_swizzle_enabled();
+
 // Temporal blocking: one sweep computes layers m (C) and m+1 (D) from A = u^{m-1} and
 // B = u^{m-2} (unused when m == 1), D-boxes as for launch_step. C is evaluated on a one-node
 // ring around every tile (redundantly, bitwise identical), inside `cdom` in j/k and as 0 on
@@ -117,8 +121,10 @@ struct SeamAlias {
     const T* prev = nullptr;
 };
 
+// `rows` per lane x `waves` wave64s per workgroup = tile height (tb2_supported()).
+bool tb2_supported(int rows, int waves);
 template <class T>
-void launch_tb2(int rows, bool first, const T* A, const T* B, T* C, T* D, const GridView& gv,
+void launch_tb2(int rows, int waves, bool first, const T* A, const T* B, T* C, T* D, const GridView& gv,
                 const Box* boxes, int nbox, const Box& cdom, int ei0, int ei1, const Wrap& wrapC,
                 const Wrap& wrapD, const SeamAlias<T>& alias, const T* tx, const T* ty,
                 const T* tz, const StepCoefs& cC, const StepCoefs& cD, u64* errC, u64* errD,

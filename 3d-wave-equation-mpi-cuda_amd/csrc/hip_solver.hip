@@ -36,6 +36,29 @@ namespace {
 
 using clk = std::chrono::steady_clock;
 
+// Temporal-blocking variant names: "tb2" (2 rows/lane, 4 waves), "tb2r<R>", "tb2r<R>w<W>".
+void parse_tb_name(const std::string& name, int& rows, int& waves) {
+    rows = 2, waves = 4;
+    std::string s = name.substr(3);
+    if (!s.empty() && s[0] == 'r') {
+        size_t n = 0;
+        rows = std::stoi(s.substr(1), &n);
+        s = s.substr(1 + n);
+    }
+    if (!s.empty() && s[0] == 'w') {
+        size_t n = 0;
+        waves = std::stoi(s.substr(1), &n);
+        s = s.substr(1 + n);
+    }
+    W3D_REQUIRE(s.empty() && tb2_supported(rows, waves), "wave3d: unknown kernel variant " + name);
+}
+
+std::string tb_name(int rows, int waves) {
+    std::string s = rows == 2 && waves == 4 ? "tb2" : "tb2r" + std::to_string(rows);
+    if (waves != 4) s += "w" + std::to_string(waves);
+    return s;
+}
+
 template <class T>
 struct DevRank {
     Topology topo;
@@ -85,13 +108,14 @@ public:
             world_ = std::max(1, c.ranks);
             for (int r = 0; r < world_; ++r) local_.push_back(r);
         }
-        // "auto": temporal blocking (tb2r4, measured fastest on MI355X, profiles/) whenever the
+        // "auto": temporal blocking (tb2, chunk 96, measured fastest on MI355X, profiles/) whenever the
         // decomposition allows it (one rank, or x slabs); otherwise the single-step march2.
         const bool yz_split = (c.dims[1] > 1 || c.dims[2] > 1);
         const bool auto_tb = c.kernel == "auto" && !yz_split;
-        tb_ = auto_tb || c.kernel == "tb2" || c.kernel == "tb2r4" || c.kernel == "tb2r8";
-        tb_rows_ = (auto_tb || c.kernel == "tb2r4") ? 4 : (c.kernel == "tb2r8" ? 8 : 2);
-        if (tb_ && cfg_.chunk == 0) cfg_.chunk = 48;
+        tb_ = auto_tb || c.kernel.rfind("tb2", 0) == 0;
+        if (auto_tb) tb_rows_ = 2, tb_waves_ = 4;
+        else if (tb_) parse_tb_name(c.kernel, tb_rows_, tb_waves_);
+        if (tb_ && cfg_.chunk == 0) cfg_.chunk = 96;
         kind_ = parse_kernel_variant(tb_ ? std::string("auto") : c.kernel);
         naive_.march = false;
         G_ = tb_ ? 2 : 1;
@@ -124,8 +148,7 @@ public:
         res.Np = world_;
         res.dtype = cfg_.dtype;
         res.backend = "hip";
-        res.kernel = tb_ ? (tb_rows_ == 2 ? std::string("tb2") : "tb2r" + std::to_string(tb_rows_))
-                         : kernel_variant_name(kind_);
+        res.kernel = tb_ ? tb_name(tb_rows_, tb_waves_) : kernel_variant_name(kind_);
         res.courant = prob_.courant;
         res.transport = ext_ ? ext_->name() : (world_ > 1 ? "loopback" : "self");
         for (int a = 0; a < 3; ++a) res.dims[a] = ranks_[0].topo.dims[a];
@@ -425,7 +448,7 @@ private:
             al.prev = R.alias_buf + R.plane_off;
         }
         if (!boxes) boxes = &R.compute, nbox = 1;
-        launch_tb2<T>(tb_rows_, m == 1, A, B, R.g[lvl(m)], R.g[lvl(m + 1)], R.gv, boxes, nbox,
+        launch_tb2<T>(tb_rows_, tb_waves_, m == 1, A, B, R.g[lvl(m)], R.g[lvl(m + 1)], R.gv, boxes, nbox,
                       R.cdom, R.error.i0, R.error.i1, R.wrap, R.wrap2, al, R.tx, R.ty, R.tz,
                       coefs(m), coefs(m + 1), R.err + size_t(m) * kSlotsPerLayer,
                       R.err + size_t(m + 1) * kSlotsPerLayer, cfg_.chunk, s);
@@ -786,6 +809,7 @@ private:
     KernelVariant kind_, naive_;
     bool tb_ = false;   // temporal blocking (2 layers per sweep)
     int tb_rows_ = 2;
+    int tb_waves_ = 4;
     int G_ = 1;         // ghost depth
     int L_ = 3;         // time levels kept
     bool overlap_ = false;

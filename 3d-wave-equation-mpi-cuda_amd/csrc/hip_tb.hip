@@ -5,7 +5,7 @@
 // (24 B fp64). One sweep here reads A = u^{m-1}, B = u^{m-2} and writes C = u^m and
 // D = u^{m+1}: 32 B per two layers = 16 B per layer.
 //
-// Workgroup = 4 wave64s owning a (4R rows) x 64 tile of D that marches along i. Per plane i:
+// Workgroup = NW wave64s owning a (NW*R rows) x 64 tile of D that marches along i. Per plane i:
 //   1. the A(i) tile plus a 2-node ring goes to LDS (own values from registers, ring from
 //      L2), one barrier;
 //   2. C(i) is computed on the tile plus a 1-node ring (redundantly with the neighbour
@@ -23,6 +23,7 @@
 
 #include <algorithm>
 #include <climits>
+#include <type_traits>
 
 #include "device_common.hpp"
 
@@ -31,6 +32,7 @@ namespace {
 
 template <class T>
 struct TbParams {
+    int xcd;  // XCD-aware tile order (xcd_swizzle)
     const T* A;
     const T* B;
     T* C;
@@ -43,8 +45,10 @@ struct TbParams {
     int nbox;
     BoxLaunch box[kMaxBoxes];
     int ei0, ei1;
-    int wc_src[kMaxWrap], wc_dst[kMaxWrap];
-    int wd_src[kMaxWrap], wd_dst[kMaxWrap];
+    // periodic self-wrap as <= 2 plane ranges with a constant shift: plane i in [lo, hi] is
+    // also stored to plane i + sh (fewer live scalars than a per-plane table)
+    int wc_lo[2], wc_hi[2], wc_sh[2];
+    int wd_lo[2], wd_hi[2], wd_sh[2];
     int an_i, ap_i;
     const T* an;
     const T* ap;
@@ -57,16 +61,25 @@ struct TbParams {
     u64* errD;
 };
 
-template <class T, bool FIRST, int R>
-__global__ void __launch_bounds__(kThreads) k_tb2(const TbParams<T> p) {
-    constexpr int TJ = kWaves * R;
+template <int V>
+using Ph = std::integral_constant<int, V>;
+
+// Rolling state lives in fixed slots indexed by plane number mod 4 (A, C) or mod 2 (B, outer
+// ring, LDS buffers) and the i loop is unrolled by 4 with the phase as a compile-time
+// constant, so no value ever moves between registers: a prefetch load lands in the slot it
+// is consumed from two planes later, and the compiler needs no s_waitcnt vmcnt(0) to copy
+// an in-flight register (the rotate-by-copy form serialised every plane on load latency).
+template <class T, bool FIRST, int R, int NW>
+__global__ void __launch_bounds__(NW * 64) k_tb2(const TbParams<T> p) {
+    constexpr int TJ = NW * R;
     constexpr int AH = TJ + 4, AW = kTK + 4;  // A tile: rows jt-2..jt+TJ+1, cols kb-2..kb+65
     constexpr int CH = TJ + 2, CW = kTK + 2;  // C tile: rows jt-1..jt+TJ,   cols kb-1..kb+64
     constexpr unsigned ES = sizeof(T);
+    static_assert(128 + 2 * CH <= NW * 64 && 132 + 2 * CH <= NW * 64, "ring needs more lanes");
     __shared__ T ldsA[2][AH][AW];
     __shared__ T ldsC[2][CH][CW];
 
-    const int bid = blockIdx.x;
+    const int bid = xcd_swizzle(blockIdx.x, gridDim.x, p.xcd);
     const int b = find_box(p, bid);
     const BoxLaunch Bx = p.box[b];
     int local = bid - Bx.block_begin;
@@ -135,135 +148,165 @@ __global__ void __launch_bounds__(kThreads) k_tb2(const TbParams<T> p) {
     }
     const unsigned ua_off = boff(uj, uk, uon && inb(uj, uk));
 
-    // rolling registers: own A at i-1, i, i+1 (+ i+2 in flight), C at i-2..i; B per plane
-    T aP[R], aC[R], aN[R], c2[R], c1[R], c0[R];
+    // Slots (iteration i = ib - 1 + q, phase P = q & 3):
+    //   A(x), ring A(x): slot (x - ib + 2) & 3 -> A(i-1) = P, A(i) = P+1, A(i+1) = P+2, A(i+2) = P+3
+    //   C(x):            slot (x - ib + 1) & 3 -> C(i) = P, C(i-1) = P+3, C(i-2) = P+2
+    //   B(x), ring B(x), outer A(x), LDS buffer: (x - ib + 1) & 1
+    T a[4][R], c[4][R], bb[2][R];
+    T ra[4], rb[2], ua[2];
     {
         const auto r0 = prs(p.A, ib - 2), r1 = prs(p.A, ib - 1), r2 = prs(p.A, ib);
+        const auto rB = prs(p.B, ib - 1);
 #pragma unroll
         for (int r = 0; r < R; ++r) {
-            aP[r] = bld<T>(r0, oa[r]);
-            aC[r] = bld<T>(r1, oa[r]);
-            aN[r] = bld<T>(r2, oa[r]);
-            c2[r] = c1[r] = c0[r] = T(0);
+            a[0][r] = bld<T>(r0, oa[r]);
+            a[1][r] = bld<T>(r1, oa[r]);
+            a[2][r] = bld<T>(r2, oa[r]);
+            a[3][r] = T(0);
+            bb[0][r] = bld<T>(rB, ob[r]);
+            bb[1][r] = T(0);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) c[q][r] = T(0);
         }
+        ra[0] = bld<T>(r0, ra_off);
+        ra[1] = bld<T>(r1, ra_off);
+        ra[2] = bld<T>(r2, ra_off);
+        ra[3] = T(0);
+        rb[0] = bld<T>(rB, rb_off);
+        rb[1] = T(0);
+        ua[0] = bld<T>(r1, ua_off);
+        ua[1] = T(0);
     }
-    T raP = bld<T>(prs(p.A, ib - 2), ra_off);
-    T raC = bld<T>(prs(p.A, ib - 1), ra_off);
-    T raN = bld<T>(prs(p.A, ib), ra_off);
-    T ua = bld<T>(prs(p.A, ib - 1), ua_off);
 
     T ma1 = T(kErrInit), mr1 = T(kErrInit), ma2 = T(kErrInit), mr2 = T(kErrInit);
     bool bad1 = false, bad2 = false;
-    int buf = 0;
 
-    for (int i = ib - 1; i <= ie + 1; ++i) {
-        // prefetch A(i+2) (own, ring) and A(i+1) (outer); B(i) now, used after the barrier
+    // prefetch A(i+2) (own, ring), A(i+1) (outer ring), B(i+1); on the last plane the
+    // descriptors get 0 records, so the loads return 0 without touching memory (uniform,
+    // no per-lane masking)
+    auto prefetch = [&](auto phase, const int i) {
+        constexpr int P = decltype(phase)::value;
+        constexpr int S3 = (P + 3) & 3, H1 = (P + 1) & 1;
         const bool more = i <= ie;
-        const auto rA2 = prs(p.A, more ? i + 2 : i);
-        const auto rA1 = prs(p.A, more ? i + 1 : i);
-        const auto rB = prs(p.B, i);
-        T aNN[R], bC[R];
+        const unsigned nb = more ? pbytes : 0u;
+        const int d2 = more ? 2 : 0, d1 = more ? 1 : 0;
+        const auto rA2 = plane_rsrc(p.A + (i64(i + d2) * si - p.poff), nb);
+        const auto rA1 = plane_rsrc(p.A + (i64(i + d1) * si - p.poff), nb);
+        const auto rB1 = plane_rsrc(p.B + (i64(i + d1) * si - p.poff), nb);
 #pragma unroll
         for (int r = 0; r < R; ++r) {
-            aNN[r] = bld<T>(rA2, more ? oa[r] : kOOB);
-            bC[r] = bld<T>(rB, ob[r]);
+            a[S3][r] = bld<T>(rA2, oa[r]);
+            bb[H1][r] = bld<T>(rB1, ob[r]);
         }
-        const T raNN = bld<T>(rA2, more ? ra_off : kOOB);
-        const T rbC = bld<T>(rB, rb_off);
-        const T uaN = bld<T>(rA1, more ? ua_off : kOOB);
+        ra[S3] = bld<T>(rA2, ra_off);
+        rb[H1] = bld<T>(rB1, rb_off);
+        ua[H1] = bld<T>(rA1, ua_off);
+    };
 
-        // 1. stage A(i)
+    // stage A(i) (own from registers, rings from the prefetch) into LDS buffer (i - ib + 1) & 1
+    auto stage = [&](auto phase) {
+        constexpr int P = decltype(phase)::value;
+        constexpr int S1 = (P + 1) & 3, H0 = P & 1;
 #pragma unroll
-        for (int r = 0; r < R; ++r) ldsA[buf][2 + w * R + r][2 + lane] = aC[r];
-        if (ron) ldsA[buf][rj - jt + 2][rk - kb + 2] = raC;
-        if (uon) ldsA[buf][uj - jt + 2][uk - kb + 2] = ua;
-        __syncthreads();
+        for (int r = 0; r < R; ++r) ldsA[H0][2 + w * R + r][2 + lane] = a[S1][r];
+        if (ron) ldsA[H0][rj - jt + 2][rk - kb + 2] = ra[S1];
+        if (uon) ldsA[H0][uj - jt + 2][uk - kb + 2] = ua[H0];
+    };
 
-        // seam aliases (uniform): x+ / x- neighbour of C(i) from another plane
-        const bool use_an = i == p.an_i, use_ap = i == p.ap_i;
-        T xnA[R], xpA[R], rxn = raN, rxp = raP;
+    // C(i) and D(i-1). ALIAS: this plane is a periodic seam, where C(i)'s x+ / x- neighbour
+    // comes from another plane (SeamAlias). A separate instantiation, so the common path
+    // never merges a conditionally loaded register (that would force s_waitcnt vmcnt(0)).
+    auto compute = [&](auto phase, auto alias, const int i) {
+        constexpr int P = decltype(phase)::value;
+        constexpr bool ALIAS = decltype(alias)::value;
+        constexpr int S0 = P & 3, S1 = (P + 1) & 3, S2 = (P + 2) & 3, S3 = (P + 3) & 3;
+        constexpr int H0 = P & 1, H1 = (P + 1) & 1;
+        T xnA[R], xpA[R], rxn = ra[S2], rxp = ra[S0];
 #pragma unroll
-        for (int r = 0; r < R; ++r) xnA[r] = aN[r], xpA[r] = aP[r];
-        if (use_an) {
-            const auto ra = plane_rsrc(p.an - p.poff, pbytes);
+        for (int r = 0; r < R; ++r) xnA[r] = a[S2][r], xpA[r] = a[S0][r];
+        if (ALIAS && i == p.an_i) {
+            const auto rs = plane_rsrc(p.an - p.poff, pbytes);
 #pragma unroll
-            for (int r = 0; r < R; ++r) xnA[r] = bld<T>(ra, oa[r]);
-            rxn = bld<T>(ra, ra_off);
+            for (int r = 0; r < R; ++r) xnA[r] = bld<T>(rs, oa[r]);
+            rxn = bld<T>(rs, ra_off);
         }
-        if (use_ap) {
-            const auto ra = plane_rsrc(p.ap - p.poff, pbytes);
+        if (ALIAS && i == p.ap_i) {
+            const auto rs = plane_rsrc(p.ap - p.poff, pbytes);
 #pragma unroll
-            for (int r = 0; r < R; ++r) xpA[r] = bld<T>(ra, oa[r]);
-            rxp = bld<T>(ra, ra_off);
+            for (int r = 0; r < R; ++r) xpA[r] = bld<T>(rs, oa[r]);
+            rxp = bld<T>(rs, ra_off);
         }
 
-        // 2. C(i) on own nodes and the ring (0 on Dirichlet faces)
+        // C(i) on own nodes and the ring (0 on Dirichlet faces)
 #pragma unroll
         for (int r = 0; r < R; ++r) {
-            const int ra = 2 + w * R + r, ca = 2 + lane;
-            const T lap = laplace7_cr(aC[r], xpA[r], xnA[r], ldsA[buf][ra - 1][ca], ldsA[buf][ra + 1][ca],
-                                      ldsA[buf][ra][ca - 1], ldsA[buf][ra][ca + 1], p.hx2, p.hy2,
-                                      p.hz2, p.yx2, p.yy2, p.yz2);
-            const T cv = FIRST ? taylor_first(aC[r], lap, p.coefC) : leapfrog(aC[r], bC[r], lap, p.coefC);
-            c0[r] = ocd[r] ? cv : T(0);
-            ldsC[buf][1 + w * R + r][1 + lane] = c0[r];
+            const int ya = 2 + w * R + r, xa = 2 + lane;
+            const T lap = laplace7_cr(a[S1][r], xpA[r], xnA[r], ldsA[H0][ya - 1][xa],
+                                      ldsA[H0][ya + 1][xa], ldsA[H0][ya][xa - 1],
+                                      ldsA[H0][ya][xa + 1], p.hx2, p.hy2, p.hz2, p.yx2, p.yy2,
+                                      p.yz2);
+            const T cv = FIRST ? taylor_first(a[S1][r], lap, p.coefC)
+                               : leapfrog(a[S1][r], bb[H0][r], lap, p.coefC);
+            c[S0][r] = ocd[r] ? cv : T(0);
+            ldsC[H0][1 + w * R + r][1 + lane] = c[S0][r];
         }
         if (ron) {
-            const int ra = rj - jt + 2, ca = rk - kb + 2;
-            const T lap = laplace7_cr(raC, rxp, rxn, ldsA[buf][ra - 1][ca], ldsA[buf][ra + 1][ca],
-                                      ldsA[buf][ra][ca - 1], ldsA[buf][ra][ca + 1], p.hx2, p.hy2,
+            const int ya = rj - jt + 2, xa = rk - kb + 2;
+            const T lap = laplace7_cr(ra[S1], rxp, rxn, ldsA[H0][ya - 1][xa], ldsA[H0][ya + 1][xa],
+                                      ldsA[H0][ya][xa - 1], ldsA[H0][ya][xa + 1], p.hx2, p.hy2,
                                       p.hz2, p.yx2, p.yy2, p.yz2);
-            const T cv = FIRST ? taylor_first(raC, lap, p.coefC) : leapfrog(raC, rbC, lap, p.coefC);
-            ldsC[buf][ra - 1][ca - 1] = rcd ? cv : T(0);
+            const T cv = FIRST ? taylor_first(ra[S1], lap, p.coefC)
+                               : leapfrog(ra[S1], rb[H0], lap, p.coefC);
+            ldsC[H0][ya - 1][xa - 1] = rcd ? cv : T(0);
         }
 
         // own C(i): store, wrap, error (only the work item's own planes)
         if (i >= ib && i <= ie) {
-            const bool erow = i >= p.ei0 && i <= p.ei1;
-            const T sx = p.tx[i];
             const auto rc = prs(p.C, i);
 #pragma unroll
-            for (int r = 0; r < R; ++r) bst(c0[r], rc, os[r]);
+            for (int r = 0; r < R; ++r) bst(c[S0][r], rc, os[r]);
 #pragma unroll
-            for (int q = 0; q < kMaxWrap; ++q)
-                if (i == p.wc_src[q]) {
-                    const auto rw = prs(p.C, p.wc_dst[q]);
+            for (int g = 0; g < 2; ++g)
+                if (i >= p.wc_lo[g] && i <= p.wc_hi[g]) {
+                    const auto rw = prs(p.C, i + p.wc_sh[g]);
 #pragma unroll
-                    for (int r = 0; r < R; ++r) bst(c0[r], rw, os[r]);
+                    for (int r = 0; r < R; ++r) bst(c[S0][r], rw, os[r]);
                 }
+            const bool erow = i >= p.ei0 && i <= p.ei1;
+            const T sx = ldconst(p.tx, i);
 #pragma unroll
             for (int r = 0; r < R; ++r) {
                 if (!ovalid[r]) continue;
-                bad1 |= nonfinite(c0[r]);
-                if (erow) accumulate_error(c0[r], analytic(sx, oty[r], otz, p.ctC), ma1, mr1);
+                bad1 |= nonfinite(c[S0][r]);
+                if (erow) accumulate_error(c[S0][r], analytic(sx, oty[r], otz, p.ctC), ma1, mr1);
             }
         }
 
-        // 3. D(i-1) from the C(i-1) tile (written last iteration, other buffer)
+        // D(i-1) from the C(i-1) tile (written last iteration, other buffer)
         const int id = i - 1;
         if (id >= ib && id <= ie) {
-            const bool erow = id >= p.ei0 && id <= p.ei1;
-            const T sx = p.tx[id];
-            const int pb = buf ^ 1;
             T dv[R];
 #pragma unroll
             for (int r = 0; r < R; ++r) {
-                const int rc = 1 + w * R + r, cc = 1 + lane;
-                const T lap = laplace7_cr(c1[r], c2[r], c0[r], ldsC[pb][rc - 1][cc], ldsC[pb][rc + 1][cc],
-                                          ldsC[pb][rc][cc - 1], ldsC[pb][rc][cc + 1], p.hx2, p.hy2,
-                                          p.hz2, p.yx2, p.yy2, p.yz2);
-                dv[r] = leapfrog(c1[r], aP[r], lap, p.coefD);
+                const int yc = 1 + w * R + r, xc = 1 + lane;
+                const T lap = laplace7_cr(c[S3][r], c[S2][r], c[S0][r], ldsC[H1][yc - 1][xc],
+                                          ldsC[H1][yc + 1][xc], ldsC[H1][yc][xc - 1],
+                                          ldsC[H1][yc][xc + 1], p.hx2, p.hy2, p.hz2, p.yx2,
+                                          p.yy2, p.yz2);
+                dv[r] = leapfrog(c[S3][r], a[S0][r], lap, p.coefD);
             }
             const auto rd = prs(p.D, id);
 #pragma unroll
             for (int r = 0; r < R; ++r) bst(dv[r], rd, os[r]);
 #pragma unroll
-            for (int q = 0; q < kMaxWrap; ++q)
-                if (id == p.wd_src[q]) {
-                    const auto rw = prs(p.D, p.wd_dst[q]);
+            for (int g = 0; g < 2; ++g)
+                if (id >= p.wd_lo[g] && id <= p.wd_hi[g]) {
+                    const auto rw = prs(p.D, id + p.wd_sh[g]);
 #pragma unroll
                     for (int r = 0; r < R; ++r) bst(dv[r], rw, os[r]);
                 }
+            const bool erow = id >= p.ei0 && id <= p.ei1;
+            const T sx = ldconst(p.tx, id);
 #pragma unroll
             for (int r = 0; r < R; ++r) {
                 if (!ovalid[r]) continue;
@@ -271,39 +314,87 @@ __global__ void __launch_bounds__(kThreads) k_tb2(const TbParams<T> p) {
                 if (erow) accumulate_error(dv[r], analytic(sx, oty[r], otz, p.ctD), ma2, mr2);
             }
         }
+    };
 
-        // roll
-#pragma unroll
-        for (int r = 0; r < R; ++r) {
-            aP[r] = aC[r];
-            aC[r] = aN[r];
-            aN[r] = aNN[r];
-            c2[r] = c1[r];
-            c1[r] = c0[r];
-        }
-        raP = raC;
-        raC = raN;
-        raN = raNN;
-        ua = uaN;
-        buf ^= 1;
+    auto plane = [&](auto phase, const int i) {
+        prefetch(phase, i);
+        stage(phase);
+        __syncthreads();
+        if (i == p.an_i || i == p.ap_i) compute(phase, std::true_type{}, i);
+        else compute(phase, std::false_type{}, i);
+    };
+
+    // i = ib-1 .. ie+1 (>= 3 planes), unrolled by 4 so every slot index is a constant
+    for (int i = ib - 1;;) {
+        plane(Ph<0>{}, i);
+        if (++i > ie + 1) break;
+        plane(Ph<1>{}, i);
+        if (++i > ie + 1) break;
+        plane(Ph<2>{}, i);
+        if (++i > ie + 1) break;
+        plane(Ph<3>{}, i);
+        if (++i > ie + 1) break;
     }
-    commit_errors(ma1, mr1, bad1, p.errC);
+    commit_errors<T, NW>(ma1, mr1, bad1, p.errC);
     __syncthreads();
-    commit_errors(ma2, mr2, bad2, p.errD);
+    commit_errors<T, NW>(ma2, mr2, bad2, p.errD);
+}
+
+// Wrap table -> <= 2 (lo, hi, shift) plane ranges.
+void wrap_ranges(const Wrap& w, int lo[2], int hi[2], int sh[2]) {
+    int n = 0;
+    lo[0] = lo[1] = INT_MAX;
+    hi[0] = hi[1] = INT_MIN;
+    sh[0] = sh[1] = 0;
+    for (int q = 0; q < kMaxWrap; ++q) {
+        if (w.src[q] < 1) continue;
+        const int s = w.dst[q] - w.src[q];
+        int g = 0;
+        for (; g < n; ++g)
+            if (sh[g] == s && (w.src[q] == hi[g] + 1 || w.src[q] == lo[g] - 1)) break;
+        if (g == n) {
+            W3D_REQUIRE(n < 2, "tb2: self-wrap needs more than two plane ranges");
+            ++n;
+            sh[g] = s;
+            lo[g] = hi[g] = w.src[q];
+        }
+        lo[g] = std::min(lo[g], w.src[q]);
+        hi[g] = std::max(hi[g], w.src[q]);
+    }
 }
 
 }  // namespace
 
+template <class T, bool F>
+static void (*tb_kernel(int rows, int waves))(const TbParams<T>) {
+    switch (rows * 100 + waves) {
+        case 204: return k_tb2<T, F, 2, 4>;
+        case 404: return k_tb2<T, F, 4, 4>;
+        case 804: return k_tb2<T, F, 8, 4>;
+        case 208: return k_tb2<T, F, 2, 8>;
+        case 408: return k_tb2<T, F, 4, 8>;
+        case 216: return k_tb2<T, F, 2, 16>;
+        default: throw Error("tb2: unsupported rows x waves " + std::to_string(rows) + "x" +
+                             std::to_string(waves));
+    }
+}
+
+bool tb2_supported(int rows, int waves) {
+    const int c = rows * 100 + waves;
+    return c == 204 || c == 404 || c == 804 || c == 208 || c == 408 || c == 216;
+}
+
 template <class T>
-void launch_tb2(int rows, bool first, const T* A, const T* B, T* C, T* D, const GridView& gv,
+void launch_tb2(int rows, int waves, bool first, const T* A, const T* B, T* C, T* D, const GridView& gv,
                 const Box* boxes, int nbox, const Box& cdom, int ei0, int ei1, const Wrap& wrapC,
                 const Wrap& wrapD, const SeamAlias<T>& alias, const T* tx, const T* ty,
                 const T* tz, const StepCoefs& cC, const StepCoefs& cD, u64* errC, u64* errD,
                 int chunk, hipStream_t s) {
     W3D_REQUIRE(gv.G >= 2, "temporal blocking needs ghost depth >= 2");
-    W3D_REQUIRE(rows == 2 || rows == 4 || rows == 8, "tb2 rows per lane must be 2, 4 or 8");
+    W3D_REQUIRE(tb2_supported(rows, waves), "tb2: unsupported rows x waves");
     W3D_REQUIRE(nbox >= 1 && nbox <= kMaxBoxes, "bad box count");
     TbParams<T> p{};
+    p.xcd = xcd_swizzle_enabled();
     p.A = A;
     p.B = B;
     p.C = C;
@@ -321,10 +412,8 @@ void launch_tb2(int rows, bool first, const T* A, const T* B, T* C, T* D, const 
     p.ck1 = cdom.k1;
     p.ei0 = ei0;
     p.ei1 = ei1;
-    for (int q = 0; q < kMaxWrap; ++q) {
-        p.wc_src[q] = wrapC.src[q], p.wc_dst[q] = wrapC.dst[q];
-        p.wd_src[q] = wrapD.src[q], p.wd_dst[q] = wrapD.dst[q];
-    }
+    wrap_ranges(wrapC, p.wc_lo, p.wc_hi, p.wc_sh);
+    wrap_ranges(wrapD, p.wd_lo, p.wd_hi, p.wd_sh);
     p.an_i = alias.next ? alias.next_i : INT_MIN;
     p.ap_i = alias.prev ? alias.prev_i : INT_MIN;
     p.an = alias.next;
@@ -344,7 +433,7 @@ void launch_tb2(int rows, bool first, const T* A, const T* B, T* C, T* D, const 
     p.ctD = T(cD.ct);
     p.errC = errC;
     p.errD = errD;
-    const int TJ = kWaves * rows;
+    const int TJ = waves * rows;
     int nb = 0, total = 0;
     for (int q = 0; q < nbox; ++q) {
         const Box& bx = boxes[q];
@@ -359,23 +448,21 @@ void launch_tb2(int rows, bool first, const T* A, const T* B, T* C, T* D, const 
         L.tiles_k = t1 - t0 + 1;
         L.tiles_j = cdiv(bx.j1 - bx.j0 + 1, TJ);
         const int planes = bx.i1 - bx.i0 + 1;
-        L.chunk = std::min(chunk > 0 ? chunk : 32, planes);
+        const int want = std::min(chunk > 0 ? chunk : 96, planes);
+        L.chunk = cdiv(planes, cdiv(planes, want));  // equal work items (no short tail chunk)
         L.block_begin = total;
         total += L.tiles_k * L.tiles_j * cdiv(planes, L.chunk);
         ++nb;
     }
     p.nbox = nb;
     if (nb == 0) return;
-    void (*kern)(const TbParams<T>);
-    if (rows == 2) kern = first ? k_tb2<T, true, 2> : k_tb2<T, false, 2>;
-    else if (rows == 8) kern = first ? k_tb2<T, true, 8> : k_tb2<T, false, 8>;
-    else kern = first ? k_tb2<T, true, 4> : k_tb2<T, false, 4>;
-    hipLaunchKernelGGL(kern, dim3(total), dim3(kThreads), 0, s, p);
+    auto kern = first ? tb_kernel<T, true>(rows, waves) : tb_kernel<T, false>(rows, waves);
+    hipLaunchKernelGGL(kern, dim3(total), dim3(waves * 64), 0, s, p);
     HIP_OK(hipGetLastError());
 }
 
 #define W3D_TB_INST(T)                                                                       \
-    template void launch_tb2<T>(int, bool, const T*, const T*, T*, T*, const GridView&,      \
+    template void launch_tb2<T>(int, int, bool, const T*, const T*, T*, T*, const GridView&,      \
                                 const Box*, int, const Box&, int, int, const Wrap&,          \
                                 const Wrap&, const SeamAlias<T>&, const T*, const T*,        \
                                 const T*, const StepCoefs&, const StepCoefs&, u64*, u64*,    \

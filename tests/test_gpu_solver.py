@@ -21,13 +21,13 @@ def _fmt(r):
     return [(fmt6(a), fmt6(b)) for a, b in zip(r.max_abs, r.max_rel)]
 
 
-@pytest.mark.parametrize("kernel", ["march", "naive", "auto", "march8", "tb2", "tb2r4"])
+@pytest.mark.parametrize("kernel", ["march", "naive", "auto", "march8", "tb2", "tb2r4", "tb2r4w8", "tb2r2w16"])
 def test_golden_n32(C, kernel):
     import wave3d
     from wave3d.utils import GOLDEN_N32_K20
 
     r = _solve(wave3d.WaveProblem(32, timesteps=20), kernel=kernel)
-    assert r.backend == "hip" and r.kernel == {"march": "march4", "auto": "tb2r4"}.get(kernel, kernel)
+    assert r.backend == "hip" and r.kernel == {"march": "march4", "auto": "tb2"}.get(kernel, kernel)
     assert _fmt(r) == GOLDEN_N32_K20
 
 
