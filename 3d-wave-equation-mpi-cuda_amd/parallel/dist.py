@@ -12,6 +12,11 @@
   memory over gloo. Slow, but lets P processes share one GPU (RCCL refuses duplicate GPUs),
   which is how the multi-process HIP path is tested on a single MI355X — the role MPS
   oversubscription plays in the reference (README.txt:44, cuda_sol.cpp:519).
+
+Both Python transports default to ``fifo=True``: every message travels with tag 0, so
+messages between a pair of ranks match strictly in posting order — the semantics of
+tag-less ncclSend/ncclRecv. A solver whose per-peer message order were inconsistent
+between sender and receiver would fail the multi-process tests here, not only on RCCL.
 """
 from __future__ import annotations
 
@@ -77,13 +82,14 @@ _SIGN = np.uint64(1 << 63)
 class TorchHostTransport:
     """Factory for a native ``Transport`` backed by torch.distributed p2p on host memory."""
 
-    def __new__(cls, group=None):
+    def __new__(cls, group=None, fifo: bool = True):
         C = load()
 
         class _T(C.Transport):
             def __init__(self, g):
                 C.Transport.__init__(self)
                 self.g = g
+                self.fifo = fifo
 
             def name(self):
                 return "torch." + dist.get_backend(self.g)
@@ -100,9 +106,11 @@ class TorchHostTransport:
             def exchange(self, sends, recvs, stream):
                 ops = []
                 for peer, tag, addr, nb in recvs:
-                    ops.append(dist.irecv(_host_view(addr, nb), src=peer, group=self.g, tag=tag))
+                    ops.append(dist.irecv(_host_view(addr, nb), src=peer, group=self.g,
+                                          tag=0 if self.fifo else tag))
                 for peer, tag, addr, nb in sends:
-                    ops.append(dist.isend(_host_view(addr, nb), dst=peer, group=self.g, tag=tag))
+                    ops.append(dist.isend(_host_view(addr, nb), dst=peer, group=self.g,
+                                          tag=0 if self.fifo else tag))
                 for w in ops:
                     w.wait()
 
@@ -127,13 +135,14 @@ class TorchHostTransport:
 class TorchStagedTransport:
     """Factory for a device ``Transport``: D2H -> gloo p2p -> H2D (testing/bring-up only)."""
 
-    def __new__(cls, group=None):
+    def __new__(cls, group=None, fifo: bool = True):
         C = load()
 
         class _S(C.Transport):
             def __init__(self, g):
                 C.Transport.__init__(self)
                 self.g = g
+                self.fifo = fifo
 
             def name(self):
                 return "staged." + dist.get_backend(self.g)
@@ -155,9 +164,10 @@ class TorchStagedTransport:
                     C.hip_memcpy(h.ctypes.data, addr, nb, stream)
                     sbufs.append((peer, tag, torch.from_numpy(h)))
                 rbufs = [(addr, nb, torch.empty(nb, dtype=torch.uint8)) for _, _, addr, nb in recvs]
-                ops = [dist.irecv(t, src=peer, group=self.g, tag=tag)
+                tg = (lambda tag: 0) if self.fifo else (lambda tag: tag)
+                ops = [dist.irecv(t, src=peer, group=self.g, tag=tg(tag))
                        for (peer, tag, _, _), (_, _, t) in zip(recvs, rbufs)]
-                ops += [dist.isend(t, dst=peer, group=self.g, tag=tag) for peer, tag, t in sbufs]
+                ops += [dist.isend(t, dst=peer, group=self.g, tag=tg(tag)) for peer, tag, t in sbufs]
                 for w in ops:
                     w.wait()
                 for addr, nb, t in rbufs:
