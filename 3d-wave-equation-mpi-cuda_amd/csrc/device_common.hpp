@@ -4,6 +4,8 @@
 
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include "hip_kernels.hpp"
 #include "stencil_math.hpp"
 
@@ -118,6 +120,59 @@ template <class T>
 __device__ __forceinline__ T ldconst(const T* base, int i) {
     using CP = const __attribute__((address_space(4))) T*;
     return ((CP)(base))[i];
+}
+
+// compile-time loop phase (unrolled rolling-register loops)
+template <int V>
+using Ph = std::integral_constant<int, V>;
+
+// ---- row vectors: L = 1 (scalar T) or 2 (packed fp32 pair of rows) --------------------
+template <class T, int L>
+struct RowVec {
+    using type = T;
+};
+template <>
+struct RowVec<float, 2> {
+    using type = f32x2;
+};
+template <int L, class V>
+__device__ __forceinline__ auto vget(const V& v, int e) {
+    if constexpr (L == 1) return v;
+    else return v[e];
+}
+template <int L, class V, class T>
+__device__ __forceinline__ void vset(V& v, int e, T x) {
+    if constexpr (L == 1) v = x;
+    else v[e] = x;
+}
+template <int L, class V, class T>
+__device__ __forceinline__ V vsplat(T x) {
+    if constexpr (L == 1) return x;
+    else return V{x, x};
+}
+
+// Periodic self-wrap table -> <= 2 (lo, hi, shift) plane ranges (plane i in [lo, hi] is
+// also stored to plane i + shift): fewer live scalars in the kernels than a 4-entry table.
+inline void wrap_ranges(const Wrap& w, int lo[2], int hi[2], int sh[2]) {
+    int n = 0;
+    lo[0] = lo[1] = 1 << 30;
+    hi[0] = hi[1] = -(1 << 30);
+    sh[0] = sh[1] = 0;
+    for (int q = 0; q < kMaxWrap; ++q) {
+        if (w.src[q] < 1) continue;
+        const int s = w.dst[q] - w.src[q];
+        int g = 0;
+        for (; g < n; ++g)
+            if (sh[g] == s && (w.src[q] == hi[g] + 1 || w.src[q] == lo[g] - 1)) break;
+        if (g == n) {
+            W3D_REQUIRE(n < 2, "self-wrap needs more than two plane ranges");
+            ++n;
+            sh[g] = s;
+            lo[g] = hi[g] = w.src[q];
+        }
+        lo[g] = lo[g] < w.src[q] ? lo[g] : w.src[q];
+        hi[g] = hi[g] > w.src[q] ? hi[g] : w.src[q];
+    }
 }
 
 // AUX = cache policy bits of the buffer instruction (0 default, 2 = nt: read-once streams)

@@ -44,7 +44,8 @@ struct StepParams {
     int nbox;
     BoxLaunch box[kMaxBoxes];
     int ei0, ei1;
-    int wsrc[kMaxWrap], wdst[kMaxWrap];
+    int wsrc[kMaxWrap], wdst[kMaxWrap];  // k_naive
+    int w_lo[2], w_hi[2], w_sh[2];       // k_march (wrap_ranges)
     T* zbuf0;
     T* zbuf1;
     int zk0, zk1;
@@ -77,12 +78,18 @@ __device__ __forceinline__ void store_point(const StepParams<T>& p, int i, int j
 // ---------------------------------------------------------------------------------------
 // 2.5-D marching kernel (LDS tile + register-rolling i column).
 // R = rows (j) per lane; the workgroup tile is (4R) x 64. NT = non-temporal loads of the
-// read-once level u^{n-2}.
-template <class T, bool FIRST, int R, bool NT, bool FAST = false>
+// read-once level u^{n-2}. L = 2 (fp32 only): the lane's rows are processed in pairs as
+// packed fp32 (v_pk_*), halving the VALU cost of the stencil arithmetic.
+// Rolling state sits in fixed slots (plane number mod 4 / mod 2) and the i loop is unrolled
+// by 4 with the phase as a constant, so a prefetched plane is consumed from the register it
+// was loaded into (no copies of in-flight loads, no s_waitcnt vmcnt(0) per plane).
+template <class T, bool FIRST, int R, bool NT, bool FAST, int L>
 __global__ void __launch_bounds__(kThreads) k_march(const StepParams<T> p) {
-    constexpr int kRows = R;
+    using V = typename RowVec<T, L>::type;
+    constexpr int NV = R / L;
     constexpr int kTJ = kWaves * R;
     constexpr unsigned ES = sizeof(T);
+    static_assert(R % L == 0, "rows per lane must be a multiple of the vector width");
     __shared__ T lds[2][kTJ + 2][kLW];
 
     const int bid = xcd_swizzle(blockIdx.x, gridDim.x, p.xcd);
@@ -110,21 +117,19 @@ __global__ void __launch_bounds__(kThreads) k_march(const StepParams<T> p) {
     auto boff = [&](int j, int kk, bool ok) { return ok ? unsigned(j * p.sj + kk + p.poff) * ES : kOOB; };
     auto prs = [&](const T* base, int i) { return plane_rsrc(base + (i64(i) * si - p.poff), pbytes); };
 
-    int rowoff[kRows];
-    unsigned oa[kRows], ou2[kRows], os[kRows];
-    bool valid[kRows];
-    T ty[kRows];
+    unsigned oa[R], ou2[R], os[R];
+    bool valid[R];
+    V ty[NV];
 #pragma unroll
-    for (int r = 0; r < kRows; ++r) {
-        const int j = jt + w * kRows + r;
-        rowoff[r] = j * p.sj + k;
+    for (int r = 0; r < R; ++r) {
+        const int j = jt + w * R + r;
         valid[r] = kin && j <= B.j1;
         oa[r] = boff(j, k, kload && j <= p.jmax);
         ou2[r] = boff(j, k, !FIRST && valid[r]);
         os[r] = boff(j, k, valid[r]);
-        ty[r] = valid[r] ? p.ty[j] : T(0);
+        vset<L>(ty[r / L], r % L, valid[r] ? p.ty[j] : T(0));
     }
-    const T tz = kin ? p.tz[k] : T(0);
+    const V tz = vsplat<L, V>(kin ? p.tz[k] : T(0));
 
     // halo role of this lane: one LDS cell per plane
     int hrow = 0, hcol = 0;
@@ -152,101 +157,134 @@ __global__ void __launch_bounds__(kThreads) k_march(const StepParams<T> p) {
     }
     constexpr int kU2Aux = NT ? 2 : 0;  // non-temporal u^{n-2} (read once)
 
-    T Pv[kRows], Cv[kRows], Nv[kRows], U2c[kRows];
+    // slots: u1(x) -> (x - ib + 1) & 3, u2(x), halo(x), LDS buffer -> (x - ib) & 1
+    V u1[4][NV], u2[2][NV];
+    T hv[2];
     {
         const auto r0 = prs(p.u1, ib - 1), r1 = prs(p.u1, ib), r2 = prs(p.u1, ib + 1);
         const auto q0 = prs(p.u2, ib);
 #pragma unroll
-        for (int r = 0; r < kRows; ++r) {
-            Pv[r] = bld<T>(r0, oa[r]);
-            Cv[r] = bld<T>(r1, oa[r]);
-            Nv[r] = bld<T>(r2, oa[r]);
-            U2c[r] = FIRST ? T(0) : bld<T, kU2Aux>(q0, ou2[r]);
+        for (int r = 0; r < R; ++r) {
+            vset<L>(u1[0][r / L], r % L, bld<T>(r0, oa[r]));
+            vset<L>(u1[1][r / L], r % L, bld<T>(r1, oa[r]));
+            vset<L>(u1[2][r / L], r % L, bld<T>(r2, oa[r]));
+            vset<L>(u1[3][r / L], r % L, T(0));
+            vset<L>(u2[0][r / L], r % L, FIRST ? T(0) : bld<T, kU2Aux>(q0, ou2[r]));
+            vset<L>(u2[1][r / L], r % L, T(0));
         }
+        hv[0] = bld<T>(r1, hoff);
+        hv[1] = T(0);
     }
-    T H = bld<T>(prs(p.u1, ib), hoff);
+    const V hx2 = vsplat<L, V>(p.hx2), hy2 = vsplat<L, V>(p.hy2), hz2 = vsplat<L, V>(p.hz2);
+    const V yx2 = vsplat<L, V>(p.yx2), yy2 = vsplat<L, V>(p.yy2), yz2 = vsplat<L, V>(p.yz2);
+    const V coef = vsplat<L, V>(p.coef), ctv = vsplat<L, V>(p.ct);
 
     T ma = T(kErrInit), mr = T(kErrInit);
     bool bad = false;
-    int buf = 0;
-    for (int i = ib; i <= ie; ++i) {
-        // prefetch plane i+2 (own rows), plane i+1 (halo, u2)
-        T NN[kRows], U2n[kRows];
-        const bool more = i < ie;
-        const auto rN = prs(p.u1, more ? i + 2 : i);
-        const auto rH = prs(p.u1, more ? i + 1 : i);
-        const auto rU = prs(p.u2, more ? i + 1 : i);
+
+    auto plane = [&](auto phase, const int i) {
+        constexpr int P = decltype(phase)::value;
+        constexpr int S0 = P & 3, S1 = (P + 1) & 3, S2 = (P + 2) & 3, S3 = (P + 3) & 3;
+        constexpr int H0 = P & 1, H1 = (P + 1) & 1;
+        // prefetch u1(i+2) (own rows), u1(i+1) (halo), u2(i+1); 0-record descriptors on the
+        // last plane (loads return 0 without touching memory)
+        {
+            const bool more = i < ie;
+            const unsigned nb = more ? pbytes : 0u;
+            const int d2 = more ? 2 : 0, d1 = more ? 1 : 0;
+            const auto rN = plane_rsrc(p.u1 + (i64(i + d2) * si - p.poff), nb);
+            const auto rH = plane_rsrc(p.u1 + (i64(i + d1) * si - p.poff), nb);
+            const auto rU = plane_rsrc(p.u2 + (i64(i + d1) * si - p.poff), nb);
 #pragma unroll
-        for (int r = 0; r < kRows; ++r) {
-            NN[r] = bld<T>(rN, more ? oa[r] : kOOB);
-            U2n[r] = FIRST ? T(0) : bld<T, kU2Aux>(rU, more ? ou2[r] : kOOB);
+            for (int r = 0; r < R; ++r) {
+                vset<L>(u1[S3][r / L], r % L, bld<T>(rN, oa[r]));
+                if (!FIRST) vset<L>(u2[H1][r / L], r % L, bld<T, kU2Aux>(rU, ou2[r]));
+            }
+            hv[H1] = bld<T>(rH, hoff);
         }
-        const T Hn = bld<T>(rH, more ? hoff : kOOB);
 
         // stage plane i
 #pragma unroll
-        for (int r = 0; r < kRows; ++r) lds[buf][1 + w * kRows + r][1 + lane] = Cv[r];
-        if (hon) lds[buf][hrow][hcol] = H;
+        for (int r = 0; r < R; ++r) lds[H0][1 + w * R + r][1 + lane] = vget<L>(u1[S1][r / L], r % L);
+        if (hon) lds[H0][hrow][hcol] = hv[H0];
         __syncthreads();
 
-        const T sx = p.tx[i];
+        const T sx = ldconst(p.tx, i);
         const bool erow = i >= p.ei0 && i <= p.ei1;
-        T vv[kRows];
+        V vv[NV];
 #pragma unroll
-        for (int r = 0; r < kRows; ++r) {
-            const int lr = 1 + w * kRows + r;
-            const T jm = r == 0 ? lds[buf][lr - 1][1 + lane] : Cv[r - 1];
-            const T jp = r == kRows - 1 ? lds[buf][lr + 1][1 + lane] : Cv[r + 1];
-            const T km = lds[buf][lr][lane];
-            const T kp = lds[buf][lr][lane + 2];
-            if constexpr (FAST) {
-                const T lap = laplace7_fast(Cv[r], Pv[r], Nv[r], jm, jp, km, kp, p.rx2, p.ry2, p.rz2);
-                vv[r] = FIRST ? __builtin_fma(p.coef, lap, Cv[r])
-                              : __builtin_fma(p.coef, lap, T(2) * Cv[r] - U2c[r]);
+        for (int v = 0; v < NV; ++v) {
+            const int r0 = v * L, lr = 1 + w * R + r0;
+            const V c = u1[S1][v];
+            V jm, jp, km, kp;
+            if constexpr (L == 1) {
+                jm = v == 0 ? lds[H0][lr - 1][1 + lane] : u1[S1][v - 1];
+                jp = v == NV - 1 ? lds[H0][lr + 1][1 + lane] : u1[S1][v + 1];
+                km = lds[H0][lr][lane];
+                kp = lds[H0][lr][lane + 2];
             } else {
-                const T lap = laplace7_cr(Cv[r], Pv[r], Nv[r], jm, jp, km, kp, p.hx2, p.hy2, p.hz2,
-                                          p.yx2, p.yy2, p.yz2);
-                vv[r] = FIRST ? taylor_first(Cv[r], lap, p.coef) : leapfrog(Cv[r], U2c[r], lap, p.coef);
+                jm = V{v == 0 ? lds[H0][lr - 1][1 + lane] : u1[S1][v - 1][1], c[0]};
+                jp = V{c[1], v == NV - 1 ? lds[H0][lr + 2][1 + lane] : u1[S1][v + 1][0]};
+                km = V{lds[H0][lr][lane], lds[H0][lr + 1][lane]};
+                kp = V{lds[H0][lr][lane + 2], lds[H0][lr + 1][lane + 2]};
+            }
+            if constexpr (FAST) {
+                const V lap = laplace7_fast(c, u1[S0][v], u1[S2][v], jm, jp, km, kp,
+                                            vsplat<L, V>(p.rx2), vsplat<L, V>(p.ry2),
+                                            vsplat<L, V>(p.rz2));
+                vv[v] = FIRST ? __builtin_fma(p.coef, lap, c)
+                              : __builtin_fma(p.coef, lap, T(2) * c - u2[H0][v]);
+            } else {
+                const V lap = laplace7_cr(c, u1[S0][v], u1[S2][v], jm, jp, km, kp, hx2, hy2, hz2,
+                                          yx2, yy2, yz2);
+                vv[v] = FIRST ? taylor_first(c, lap, coef) : leapfrog(c, u2[H0][v], lap, coef);
             }
         }
         // stores: own plane + fused periodic wrap (buffer stores, masked lanes dropped)
         {
             const auto rs = prs(p.u, i);
 #pragma unroll
-            for (int r = 0; r < kRows; ++r) bst(vv[r], rs, os[r]);
+            for (int r = 0; r < R; ++r) bst(vget<L>(vv[r / L], r % L), rs, os[r]);
 #pragma unroll
-            for (int q = 0; q < kMaxWrap; ++q)
-                if (i == p.wsrc[q]) {
-                    const auto rw = prs(p.u, p.wdst[q]);
+            for (int g = 0; g < 2; ++g)
+                if (i >= p.w_lo[g] && i <= p.w_hi[g]) {
+                    const auto rw = prs(p.u, i + p.w_sh[g]);
 #pragma unroll
-                    for (int r = 0; r < kRows; ++r) bst(vv[r], rw, os[r]);
+                    for (int r = 0; r < R; ++r) bst(vget<L>(vv[r / L], r % L), rw, os[r]);
                 }
         }
+        const V f0 = vsplat<L, V>(sx);
 #pragma unroll
-        for (int r = 0; r < kRows; ++r) {
-            if (!valid[r]) continue;
-            const int j = jt + w * kRows + r;
-            const T v = vv[r];
-            if (k == p.zk0) p.zbuf0[i64(i - 1) * p.zrow + j] = v;
-            if (k == p.zk1) p.zbuf1[i64(i - 1) * p.zrow + j] = v;
-            if (j == p.yj0) p.ybuf0[i64(i - 1) * p.yrow + k] = v;
-            if (j == p.yj1) p.ybuf1[i64(i - 1) * p.yrow + k] = v;
-            bad |= nonfinite(v);
-            if (erow) {
-                if constexpr (FAST) accumulate_error_fast(v, analytic(sx, ty[r], tz, p.ct), ma, mr);
-                else accumulate_error(v, analytic(sx, ty[r], tz, p.ct), ma, mr);
+        for (int v = 0; v < NV; ++v) {
+            const V f = analytic(f0, ty[v], tz, ctv);
+#pragma unroll
+            for (int e = 0; e < L; ++e) {
+                const int r = v * L + e;
+                if (!valid[r]) continue;
+                const int j = jt + w * R + r;
+                const T x = vget<L>(vv[v], e);
+                if (k == p.zk0) p.zbuf0[i64(i - 1) * p.zrow + j] = x;
+                if (k == p.zk1) p.zbuf1[i64(i - 1) * p.zrow + j] = x;
+                if (j == p.yj0) p.ybuf0[i64(i - 1) * p.yrow + k] = x;
+                if (j == p.yj1) p.ybuf1[i64(i - 1) * p.yrow + k] = x;
+                bad |= nonfinite(x);
+                if (erow) {
+                    if constexpr (FAST) accumulate_error_fast(x, vget<L>(f, e), ma, mr);
+                    else accumulate_error(x, vget<L>(f, e), ma, mr);
+                }
             }
         }
-        (void)rowoff;
-#pragma unroll
-        for (int r = 0; r < kRows; ++r) {
-            Pv[r] = Cv[r];
-            Cv[r] = Nv[r];
-            Nv[r] = NN[r];
-            U2c[r] = U2n[r];
-        }
-        H = Hn;
-        buf ^= 1;
+    };
+
+    for (int i = ib;;) {
+        plane(Ph<0>{}, i);
+        if (++i > ie) break;
+        plane(Ph<1>{}, i);
+        if (++i > ie) break;
+        plane(Ph<2>{}, i);
+        if (++i > ie) break;
+        plane(Ph<3>{}, i);
+        if (++i > ie) break;
     }
     commit_errors(ma, mr, bad, p.err);
 }
@@ -377,6 +415,8 @@ bool xcd_swizzle_enabled() {
 }
 
 KernelVariant parse_kernel_variant(const std::string& name) {
+    // naive | auto | march[R][nt|f|p], R in {2,4,8} (default 4); nt = non-temporal u^{n-2},
+    // f = fast-math ablation, p = packed fp32 pairs of rows (fp32 runs only)
     KernelVariant v;
     if (name == "naive") {
         v.march = false;
@@ -386,33 +426,40 @@ KernelVariant parse_kernel_variant(const std::string& name) {
         v.rows = 2;
         return v;
     }
-    if (name == "march" || name == "march4") return v;
-    if (name == "march2") v.rows = 2;
-    else if (name == "march8") v.rows = 8;
-    else if (name == "march4nt") v.nt = true;
-    else if (name == "march2nt") v.rows = 2, v.nt = true;
-    else if (name == "march8nt") v.rows = 8, v.nt = true;
-    else if (name == "march2f") v.rows = 2, v.fast = true;
-    else if (name == "march4f") v.fast = true;
-    else throw Error("wave3d: unknown kernel variant " + name);
+    W3D_REQUIRE(name.rfind("march", 0) == 0, "wave3d: unknown kernel variant " + name);
+    std::string s = name.substr(5);
+    if (!s.empty() && (s[0] == '2' || s[0] == '4' || s[0] == '8')) v.rows = s[0] - '0', s = s.substr(1);
+    if (s == "nt") v.nt = true;
+    else if (s == "f") v.fast = true;
+    else if (s == "p") v.pk = true;
+    else W3D_REQUIRE(s.empty(), "wave3d: unknown kernel variant " + name);
+    W3D_REQUIRE(!v.fast || v.rows != 8, "wave3d: no fast-math variant with 8 rows");
+    W3D_REQUIRE(!v.pk || v.rows != 8, "wave3d: packed variants have 2 or 4 rows");
     return v;
 }
 
 std::string kernel_variant_name(const KernelVariant& v) {
     if (!v.march) return "naive";
-    return "march" + std::to_string(v.rows) + (v.nt ? "nt" : "") + (v.fast ? "f" : "");
+    return "march" + std::to_string(v.rows) + (v.nt ? "nt" : "") + (v.fast ? "f" : "") +
+           (v.pk ? "p" : "");
 }
 
 template <class T, bool FIRST>
 static void (*march_kernel(const KernelVariant& v))(const StepParams<T>) {
-    if (v.fast) return v.rows == 2 ? k_march<T, FIRST, 2, false, true> : k_march<T, FIRST, 4, false, true>;
+    if (v.pk) {
+        if constexpr (std::is_same_v<T, float>)
+            return v.rows == 2 ? k_march<T, FIRST, 2, false, false, 2> : k_march<T, FIRST, 4, false, false, 2>;
+        else throw Error("wave3d: packed march variants are fp32 only");
+    }
+    if (v.fast)
+        return v.rows == 2 ? k_march<T, FIRST, 2, false, true, 1> : k_march<T, FIRST, 4, false, true, 1>;
     switch (v.rows * 2 + (v.nt ? 1 : 0)) {
-        case 4: return k_march<T, FIRST, 2, false>;
-        case 5: return k_march<T, FIRST, 2, true>;
-        case 9: return k_march<T, FIRST, 4, true>;
-        case 16: return k_march<T, FIRST, 8, false>;
-        case 17: return k_march<T, FIRST, 8, true>;
-        default: return k_march<T, FIRST, 4, false>;
+        case 4: return k_march<T, FIRST, 2, false, false, 1>;
+        case 5: return k_march<T, FIRST, 2, true, false, 1>;
+        case 9: return k_march<T, FIRST, 4, true, false, 1>;
+        case 16: return k_march<T, FIRST, 8, false, false, 1>;
+        case 17: return k_march<T, FIRST, 8, true, false, 1>;
+        default: return k_march<T, FIRST, 4, false, false, 1>;
     }
 }
 
@@ -435,6 +482,7 @@ void launch_step(const KernelVariant& kind, bool first, const T* u1, const T* u2
     p.ei0 = ei0;
     p.ei1 = ei1;
     for (int q = 0; q < kMaxWrap; ++q) p.wsrc[q] = wrap.src[q], p.wdst[q] = wrap.dst[q];
+    wrap_ranges(wrap, p.w_lo, p.w_hi, p.w_sh);
     p.zbuf0 = pack.zbuf[0];
     p.zbuf1 = pack.zbuf[1];
     p.zk0 = pack.zbuf[0] ? pack.zk[0] : -7;

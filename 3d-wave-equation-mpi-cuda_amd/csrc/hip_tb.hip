@@ -61,9 +61,6 @@ struct TbParams {
     u64* errD;
 };
 
-template <int V>
-using Ph = std::integral_constant<int, V>;
-
 // Rolling state lives in fixed slots indexed by plane number mod 4 (A, C) or mod 2 (B, outer
 // ring, LDS buffers) and the i loop is unrolled by 4 with the phase as a compile-time
 // constant, so no value ever moves between registers: a prefetch load lands in the slot it
@@ -338,29 +335,6 @@ __global__ void __launch_bounds__(NW * 64) k_tb2(const TbParams<T> p) {
     commit_errors<T, NW>(ma1, mr1, bad1, p.errC);
     __syncthreads();
     commit_errors<T, NW>(ma2, mr2, bad2, p.errD);
-}
-
-// Wrap table -> <= 2 (lo, hi, shift) plane ranges.
-void wrap_ranges(const Wrap& w, int lo[2], int hi[2], int sh[2]) {
-    int n = 0;
-    lo[0] = lo[1] = INT_MAX;
-    hi[0] = hi[1] = INT_MIN;
-    sh[0] = sh[1] = 0;
-    for (int q = 0; q < kMaxWrap; ++q) {
-        if (w.src[q] < 1) continue;
-        const int s = w.dst[q] - w.src[q];
-        int g = 0;
-        for (; g < n; ++g)
-            if (sh[g] == s && (w.src[q] == hi[g] + 1 || w.src[q] == lo[g] - 1)) break;
-        if (g == n) {
-            W3D_REQUIRE(n < 2, "tb2: self-wrap needs more than two plane ranges");
-            ++n;
-            sh[g] = s;
-            lo[g] = hi[g] = w.src[q];
-        }
-        lo[g] = std::min(lo[g], w.src[q]);
-        hi[g] = std::max(hi[g], w.src[q]);
-    }
 }
 
 }  // namespace

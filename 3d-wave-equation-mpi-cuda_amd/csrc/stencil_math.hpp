@@ -81,6 +81,15 @@ W3D_HD void accumulate_error(T u, T f, T& mabs, T& mrel) {
 // divisions by the CPU/GPU parity tests).
 W3D_HD double fma_t(double a, double b, double c) { return __builtin_fma(a, b, c); }
 W3D_HD float fma_t(float a, float b, float c) { return __builtin_fmaf(a, b, c); }
+#ifdef __HIPCC__
+// Two fp32 lanes of one work item (two grid rows) as one packed value: v_pk_add_f32 /
+// v_pk_mul_f32 / v_pk_fma_f32 on CDNA4 — IEEE per element, so bitwise equal to two scalar
+// evaluations of the same expression.
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f32x2 fma_t(f32x2 a, f32x2 b, f32x2 c) {
+    return __builtin_elementwise_fma(a, b, c);
+}
+#endif
 
 template <class T>
 W3D_HD T div_const(T a, T b, T y) {

@@ -185,3 +185,18 @@ def test_temporal_blocking_slabs_loopback(C, ranks, overlap, kernel):
         r = _solve(p, ranks=ranks, overlap=overlap, kernel=kernel)
         assert r.dims == [ranks, 1, 1] and r.kernel == kernel
         assert r.max_abs == base.max_abs and r.max_rel == base.max_rel
+
+
+@pytest.mark.parametrize("kernel", ["march2", "march2p", "march4p", "naive", "tb2"])
+def test_fp32_bitwise_vs_cpu(C, kernel):
+    """fp32 kernels (incl. the packed-fp32 v_pk_* variants) reproduce the OpenMP fp32
+    oracle's per-layer errors bit for bit (shifted IC exercises the periodic seam)."""
+    import wave3d
+
+    p = wave3d.WaveProblem(40, timesteps=12, dtype="fp32", ic="shifted")
+    ref = _solve(p, "cpu")
+    got = _solve(p, kernel=kernel)
+    assert got.kernel == kernel
+    assert got.max_abs == ref.max_abs and got.max_rel == ref.max_rel
+    multi = _solve(p, kernel=kernel, ranks=3) if kernel != "tb2" else _solve(p, kernel=kernel, ranks=2)
+    assert multi.max_abs == ref.max_abs and multi.max_rel == ref.max_rel
