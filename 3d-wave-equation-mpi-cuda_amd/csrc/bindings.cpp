@@ -86,6 +86,7 @@ py::dict result_dict(const Config& c, const RunResult& r) {
     d["abort_reason"] = r.abort_reason;
     d["layers_done"] = r.layers_done;
     d["resumed_from"] = r.resumed_from;
+    d["graph"] = r.graph;
     d["report"] = format_report(c, r);
     d["output_file"] = output_filename(c, r);
     d["json"] = json_summary(c, r);

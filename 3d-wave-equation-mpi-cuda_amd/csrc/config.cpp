@@ -26,6 +26,7 @@ std::string usage() {
            "  --checkpoint-every k --checkpoint-dir D   --resume D\n"
            "  --repeat R --warmup W  timed / untimed solves (benchmarking)\n"
            "  --profile              per-phase timers\n"
+           "  --graph on|off|auto    replay the time loop as one hipGraph (auto: when eligible)\n"
            "  --fault SPEC           fault injection (drop_face:RANK:LAYER | nan:RANK:LAYER)\n"
            "  --device d  --threads t  --print-layers  --quiet\n";
 }
@@ -155,6 +156,12 @@ Config parse_cli(const std::vector<std::string>& a) {
             c.warmup = parse_int(need(i++), "warmup");
         } else if (o == "--profile") {
             c.profile = true;
+        } else if (o == "--graph") {
+            const std::string& v = need(i++);
+            if (v == "on") c.graph = 1;
+            else if (v == "off") c.graph = 0;
+            else if (v == "auto") c.graph = -1;
+            else throw Error("--graph must be on, off or auto");
         } else if (o == "--fault") {
             c.fault = need(i++);
         } else if (o == "--device") {

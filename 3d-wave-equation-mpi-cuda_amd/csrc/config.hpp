@@ -48,6 +48,7 @@ struct Config {
     int repeat = 1;                 // timed solves (benchmark mode)
     int warmup = 0;                 // untimed solves before the timed ones
     bool profile = false;           // per-phase hipEvent timers
+    int graph = -1;                 // hipGraph replay of the time loop: 1 on, 0 off, -1 auto
     std::string fault;              // fault injection spec, e.g. "drop_face:1:5" (or env WAVE_FI)
     int device = -1;                // explicit device id (default: local rank)
     int threads = 0;                // CPU backend OpenMP threads (0 = Np)

@@ -4,6 +4,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <type_traits>
 
 #include "hip_kernels.hpp"
@@ -103,6 +104,15 @@ __device__ __forceinline__ int find_box(const P& p, int bid) {
 }
 
 inline int cdiv(int a, int b) { return (a + b - 1) / b; }
+
+// Planes per marching work item: `best` (measured at N = 512) unless that leaves fewer than
+// ~4 workgroups per CU; then shorter chunks (>= 8 planes) trade prologue work for occupancy.
+inline int auto_chunk(int best, int planes, int tiles) {
+    constexpr int kTarget = 4 * 256;
+    int c = best;
+    if (i64(tiles) * cdiv(planes, c) < kTarget) c = std::max(8, int(i64(planes) * tiles / kTarget));
+    return std::min(std::max(1, c), planes);
+}
 
 // ---- buffer addressing (T8): wave-uniform plane descriptor + 32-bit lane byte offset -----
 // An offset >= the descriptor's byte size is out of range: loads return 0, stores are

@@ -529,9 +529,9 @@ void launch_step(const KernelVariant& kind, bool first, const T* u1, const T* u2
             if (chunk > 0) {
                 ch = std::min(chunk, planes);
             } else {
-                // 32-plane work items (chunk sweep on MI355X, profiles/): enough workgroups
-                // to balance the 256 CUs, 2 extra prologue planes per 32 computed
-                ch = std::min(32, planes);
+                // 32-plane work items (chunk sweep on MI355X, profiles/), shorter on small
+                // grids so that there are enough workgroups to fill the 256 CUs
+                ch = auto_chunk(32, planes, L.tiles_k * L.tiles_j);
             }
             ch = cdiv(planes, cdiv(planes, ch));  // equal work items (no short tail chunk)
         }

@@ -115,7 +115,6 @@ public:
         tb_ = auto_tb || c.kernel.rfind("tb2", 0) == 0;
         if (auto_tb) tb_rows_ = 2, tb_waves_ = 4;
         else if (tb_) parse_tb_name(c.kernel, tb_rows_, tb_waves_);
-        if (tb_ && cfg_.chunk == 0) cfg_.chunk = 96;
         kind_ = parse_kernel_variant(tb_ ? std::string("auto") : c.kernel);
         naive_.march = false;
         G_ = tb_ ? 2 : 1;
@@ -298,6 +297,8 @@ private:
         for (auto e : {ev_start_, ev_end_, ev_layer_, ev_halo_})
             if (e) (void)hipEventDestroy(e);
         for (auto e : prof_) (void)hipEventDestroy(e);
+        if (gexec_) (void)hipGraphExecDestroy(gexec_);
+        gexec_ = nullptr;
         s_comp_ = s_comm_ = nullptr;
     }
 
@@ -545,24 +546,75 @@ private:
         HIP_CHECK(hipStreamSynchronize(s_comp_));
         if (ext_) ext_->barrier();
 
-        auto wall0 = clk::now();
-        HIP_CHECK(hipEventRecord(ev_start_, s_comp_));
-        int start = 1;
         res.resumed_from = -1;
-        if (!cfg_.resume_dir.empty()) {
-            start = load_checkpoints() + 1;
-            res.resumed_from = start - 1;
-        } else {
-            prof_mark(s_comp_, 0);
-            for (auto& R : ranks_) {
-                launch_init<T>(R.g[0], R.gv, R.owned, tb_ ? R.wrap2 : R.wrap, R.tx, R.ty, R.tz,
-                               ct_[0], R.err, s_comp_);
-                pack_faces(R, 0, s_comp_, true);
-            }
-            prof_mark(s_comp_, 1);
-            if (K >= 1) issue_exchange(0);
-        }
         res.aborted = false;
+        if (graph_eligible() && !gexec_ && !graph_failed_) build_graph(res);  // host-only work
+        HIP_CHECK(hipEventRecord(ev_start_, s_comp_));
+        if (gexec_) {
+            // the whole IC + time loop as one graph launch (no per-kernel host overhead)
+            HIP_CHECK(hipGraphLaunch(gexec_, s_comp_));
+            res.layers_done = K;
+        } else {
+            int start = 1;
+            if (!cfg_.resume_dir.empty()) {
+                start = load_checkpoints() + 1;
+                res.resumed_from = start - 1;
+            } else {
+                enqueue_ic();
+            }
+            res.layers_done = enqueue_layers(res, start);
+        }
+        res.graph = gexec_ != nullptr;
+
+        // final max-reduction of the per-layer slots (mpi_new.cpp:358-361)
+        prof_mark(s_comp_, 4);
+        const size_t nslot = size_t(K + 1) * kSlotsPerLayer;
+        std::vector<u64> acc(nslot, 0);
+        if (ext_) {
+            HIP_CHECK(hipStreamWaitEvent(s_comp_, ev_halo_, 0));
+            ext_->allreduce_max_u64(ranks_[0].err, nslot, s_comp_);
+        }
+        for (auto& R : ranks_) {
+            HIP_CHECK(hipMemcpyAsync(host_err_.data(), R.err, nslot * sizeof(u64),
+                                     hipMemcpyDeviceToHost, s_comp_));
+            HIP_CHECK(hipStreamSynchronize(s_comp_));
+            for (size_t q = 0; q < nslot; ++q) acc[q] = std::max(acc[q], host_err_[q]);
+        }
+        prof_mark(s_comp_, 5);
+        HIP_CHECK(hipEventRecord(ev_end_, s_comp_));
+        HIP_CHECK(hipEventSynchronize(ev_end_));
+        float ms = 0;
+        HIP_CHECK(hipEventElapsedTime(&ms, ev_start_, ev_end_));
+        tm.total_ms = ms;
+        res.max_abs.assign(K + 1, kErrInit);
+        res.max_rel.assign(K + 1, kErrInit);
+        for (int n = 0; n <= K; ++n) {
+            res.max_abs[n] = decode_max_key(acc[size_t(n) * 3 + 0]);
+            res.max_rel[n] = decode_max_key(acc[size_t(n) * 3 + 1]);
+        }
+        if (res.resumed_from >= 0)
+            for (int n = 0; n <= res.resumed_from && n < int(ckpt_abs_.size()); ++n)
+                res.max_abs[n] = ckpt_abs_[n], res.max_rel[n] = ckpt_rel_[n];
+        if (cfg_.profile) collect_profile(tm);
+        else tm.loop_ms = tm.total_ms;
+    }
+
+    // ---- time loop ----------------------------------------------------------------------
+    void enqueue_ic() {
+        prof_mark(s_comp_, 0);
+        for (auto& R : ranks_) {
+            launch_init<T>(R.g[0], R.gv, R.owned, tb_ ? R.wrap2 : R.wrap, R.tx, R.ty, R.tz, ct_[0],
+                           R.err, s_comp_);
+            pack_faces(R, 0, s_comp_, true);
+        }
+        prof_mark(s_comp_, 1);
+        if (prob_.K >= 1) issue_exchange(0);
+    }
+
+    // Layers start..K on the streams; host work only for --check-every / checkpoints.
+    // Returns the last layer computed.
+    int enqueue_layers(RunResult& res, int start) {
+        const int K = prob_.K;
         int done = start - 1;
         for (int n = start; n <= K;) {
             // temporal blocking: layers n and n+1 in one sweep; a lone last layer single-step
@@ -608,40 +660,43 @@ private:
             if (ck && last < K) save_checkpoints(last);
             n += span;
         }
-        res.layers_done = done;
+        return done;
+    }
 
-        // final max-reduction of the per-layer slots (mpi_new.cpp:358-361)
-        prof_mark(s_comp_, 4);
-        const size_t nslot = size_t(K + 1) * kSlotsPerLayer;
-        std::vector<u64> acc(nslot, 0);
-        if (ext_) {
-            HIP_CHECK(hipStreamWaitEvent(s_comp_, ev_halo_, 0));
-            ext_->allreduce_max_u64(ranks_[0].err, nslot, s_comp_);
+    // hipGraph replay (HIP's answer to a tracing compiler): the IC and every layer — kernels,
+    // loopback D2D halo copies and the cross-stream event joins — are captured once per
+    // session and replayed with one hipGraphLaunch per solve. Only for runs without host
+    // interaction inside the loop (no external transport, checks, checkpoints, profiling,
+    // faults); a failed capture falls back to direct launches.
+    bool graph_eligible() const {
+        return cfg_.graph != 0 && !ext_ && cfg_.check_every == 0 && cfg_.checkpoint_every == 0 &&
+               cfg_.resume_dir.empty() && !cfg_.profile && fault_.kind.empty();
+    }
+
+    void build_graph(RunResult& res) {
+        hipGraph_t g = nullptr;
+        try {
+            HIP_CHECK(hipStreamBeginCapture(s_comp_, hipStreamCaptureModeThreadLocal));
+            enqueue_ic();
+            enqueue_layers(res, 1);
+            HIP_CHECK(hipStreamEndCapture(s_comp_, &g));
+            HIP_CHECK(hipGraphInstantiate(&gexec_, g, nullptr, nullptr, 0));
+            HIP_CHECK(hipGraphDestroy(g));
+        } catch (const Error& e) {
+            hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+            if (hipStreamIsCapturing(s_comp_, &st) == hipSuccess && st != hipStreamCaptureStatusNone) {
+                hipGraph_t h = nullptr;
+                (void)hipStreamEndCapture(s_comp_, &h);
+                if (h) (void)hipGraphDestroy(h);
+            }
+            if (g) (void)hipGraphDestroy(g);
+            (void)hipGetLastError();
+            gexec_ = nullptr;
+            graph_failed_ = true;
+            if (cfg_.graph == 1) throw;
+            if (!cfg_.quiet) std::cerr << "wave3d: hipGraph capture failed (" << e.what()
+                                       << "), using direct launches\n";
         }
-        for (auto& R : ranks_) {
-            HIP_CHECK(hipMemcpyAsync(host_err_.data(), R.err, nslot * sizeof(u64),
-                                     hipMemcpyDeviceToHost, s_comp_));
-            HIP_CHECK(hipStreamSynchronize(s_comp_));
-            for (size_t q = 0; q < nslot; ++q) acc[q] = std::max(acc[q], host_err_[q]);
-        }
-        prof_mark(s_comp_, 5);
-        HIP_CHECK(hipEventRecord(ev_end_, s_comp_));
-        HIP_CHECK(hipEventSynchronize(ev_end_));
-        float ms = 0;
-        HIP_CHECK(hipEventElapsedTime(&ms, ev_start_, ev_end_));
-        tm.total_ms = ms;
-        (void)wall0;
-        res.max_abs.assign(K + 1, kErrInit);
-        res.max_rel.assign(K + 1, kErrInit);
-        for (int n = 0; n <= K; ++n) {
-            res.max_abs[n] = decode_max_key(acc[size_t(n) * 3 + 0]);
-            res.max_rel[n] = decode_max_key(acc[size_t(n) * 3 + 1]);
-        }
-        if (res.resumed_from >= 0)
-            for (int n = 0; n <= res.resumed_from && n < int(ckpt_abs_.size()); ++n)
-                res.max_abs[n] = ckpt_abs_[n], res.max_rel[n] = ckpt_rel_[n];
-        if (cfg_.profile) collect_profile(tm);
-        else tm.loop_ms = tm.total_ms;
     }
 
     // exchange of layer n: overlapped on the comm stream, or inline on the compute stream
@@ -810,6 +865,8 @@ private:
     bool tb_ = false;   // temporal blocking (2 layers per sweep)
     int tb_rows_ = 2;
     int tb_waves_ = 4;
+    hipGraphExec_t gexec_ = nullptr;  // captured IC + time loop (graph_eligible())
+    bool graph_failed_ = false;
     int G_ = 1;         // ghost depth
     int L_ = 3;         // time levels kept
     bool overlap_ = false;

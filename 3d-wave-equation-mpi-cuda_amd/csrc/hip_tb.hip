@@ -422,7 +422,8 @@ void launch_tb2(int rows, int waves, bool first, const T* A, const T* B, T* C, T
         L.tiles_k = t1 - t0 + 1;
         L.tiles_j = cdiv(bx.j1 - bx.j0 + 1, TJ);
         const int planes = bx.i1 - bx.i0 + 1;
-        const int want = std::min(chunk > 0 ? chunk : 96, planes);
+        const int want = chunk > 0 ? std::min(chunk, planes)
+                                   : auto_chunk(96, planes, L.tiles_k * L.tiles_j);
         L.chunk = cdiv(planes, cdiv(planes, want));  // equal work items (no short tail chunk)
         L.block_begin = total;
         total += L.tiles_k * L.tiles_j * cdiv(planes, L.chunk);

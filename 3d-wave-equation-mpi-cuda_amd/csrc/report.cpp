@@ -102,7 +102,8 @@ std::string json_summary(const Config& c, const RunResult& r) {
       << ", \"max_rel_final\": " << jnum(r.max_rel.empty() ? 0.0 : r.max_rel.back())
       << ", \"solve_ms\": [";
     for (size_t i = 0; i < r.solve_ms.size(); ++i) s << (i ? ", " : "") << jnum(r.solve_ms[i]);
-    s << "], \"aborted\": " << (r.aborted ? "true" : "false") << "}";
+    s << "], \"aborted\": " << (r.aborted ? "true" : "false")
+      << ", \"graph\": " << (r.graph ? "true" : "false") << "}";
     return s.str();
 }
 

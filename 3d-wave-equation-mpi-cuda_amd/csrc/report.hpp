@@ -35,6 +35,7 @@ struct RunResult {
     int abort_layer = -1;
     std::string abort_reason;
     int resumed_from = -1;
+    bool graph = false;  // time loop replayed as one hipGraph
 
     double points() const { return double(N + 1) * double(N + 1) * double(N + 1); }
     // Mpoints/s = (N+1)^3 * timesteps / t  (BASELINE.md metric definition)

@@ -123,6 +123,7 @@ class WaveSolver:
 
     backend   "hip" (MI355X kernels) or "cpu" (OpenMP oracle)
     ranks     >0: simulate that many ranks in this process (loopback transport)
+    graph     "auto" | "on" | "off": replay the IC + time loop as one hipGraph
     transport a native transport (``parallel.rccl_transport()`` / ``TorchHostTransport``)
               making this process one rank of a distributed job
     """
@@ -132,7 +133,8 @@ class WaveSolver:
                  transport=None, Np: int | None = None, threads: int = 0, fmt: str = "none",
                  out_dir: str | None = None, check_every: int = 0, fault: str | None = None,
                  checkpoint_every: int = 0, checkpoint_dir: str | None = None,
-                 resume: str | None = None, profile: bool = False, device: int | None = None):
+                 resume: str | None = None, profile: bool = False, device: int | None = None,
+                 graph: str = "auto"):
         self.problem = problem
         self.backend = backend
         self.transport = transport
@@ -142,7 +144,7 @@ class WaveSolver:
                          out_dir=out_dir, check_every=check_every or None, fault=fault,
                          checkpoint_every=checkpoint_every or None,
                          checkpoint_dir=checkpoint_dir, resume=resume, profile=profile,
-                         device=device, quiet=True)
+                         device=device, graph=graph if backend == "hip" else None, quiet=True)
 
     def args(self, **extra) -> list[str]:
         o = dict(self.opts)

@@ -136,6 +136,7 @@ def main() -> int:
             "timesteps": a.timesteps,
             "kernel": res["kernel"],
             "overlap": not a.no_overlap,
+            "hip_graph": bool(res.get("graph", False)),
         },
         "linf_abs": res["linf_abs"],
         "linf_final_layer": res["timesteps"],

@@ -200,3 +200,16 @@ def test_fp32_bitwise_vs_cpu(C, kernel):
     assert got.max_abs == ref.max_abs and got.max_rel == ref.max_rel
     multi = _solve(p, kernel=kernel, ranks=3) if kernel != "tb2" else _solve(p, kernel=kernel, ranks=2)
     assert multi.max_abs == ref.max_abs and multi.max_rel == ref.max_rel
+
+
+@pytest.mark.parametrize("kernel,ranks", [("auto", 0), ("march2", 0), ("march2", 3), ("tb2", 2)])
+def test_graph_replay_matches_direct(C, kernel, ranks):
+    """hipGraph replay of the whole solve (incl. loopback halo copies and the overlap
+    stream joins) gives the same errors as direct launches, solve after solve."""
+    import wave3d
+
+    p = wave3d.WaveProblem(36, timesteps=11, ic="shifted")
+    d = _solve(p, kernel=kernel, ranks=ranks, graph="off")
+    g = wave3d.WaveSolver(p, "hip", kernel=kernel, ranks=ranks, graph="on").run(repeat=3)
+    assert not d.extra["graph"] and g.extra["graph"]
+    assert g.max_abs == d.max_abs and g.max_rel == d.max_rel
