@@ -13,6 +13,7 @@
 #include "hip_kernels.hpp"
 #include "problem.hpp"
 #include "rccl_transport.hpp"
+#include "sizing.hpp"
 #include "solver.hpp"
 
 namespace py = pybind11;
@@ -249,6 +250,20 @@ PYBIND11_MODULE(_wave3d_C, m) {
         return d;
     });
     m.def("usage", &usage);
+    m.def("memory_plan", [](const std::vector<std::string>& a, int world) {
+        Config c = parse_cli(a);
+        Layout l = plan_layout(c, world);
+        py::dict d;
+        d["tb"] = l.tb, d["ghost"] = l.G, d["levels"] = l.L, d["rows"] = l.rows, d["waves"] = l.waves;
+        d["dims"] = std::vector<int>{l.dims[0], l.dims[1], l.dims[2]};
+        d["bytes_per_rank"] = device_bytes_per_rank(c, world);
+        return d;
+    }, py::arg("args"), py::arg("world") = 1,
+       "Device-memory plan of the HIP solver for a CLI configuration (sizing.hpp).");
+    m.def("fill_hbm_N", [](const std::vector<std::string>& a, int world, double budget) {
+        return fill_hbm_N(parse_cli(a), world, budget);
+    }, py::arg("args"), py::arg("world"), py::arg("budget_bytes"),
+       "Largest N whose per-rank footprint fits budget_bytes (--fill-hbm).");
     m.def("topology", [](int N, int nprocs, int rank, std::vector<int> dims) {
         int d[3] = {0, 0, 0};
         for (size_t q = 0; q < dims.size() && q < 3; ++q) d[q] = dims[q];

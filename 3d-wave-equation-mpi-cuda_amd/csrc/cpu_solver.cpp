@@ -17,6 +17,7 @@
 #include <sstream>
 
 #include "checkpoint.hpp"
+#include "log.hpp"
 #include "problem.hpp"
 #include "solver.hpp"
 #include "stencil_math.hpp"
@@ -145,6 +146,9 @@ private:
         }
         ct_.clear();
         for (double v : prob_.table_t()) ct_.push_back(v);
+        for (auto& R : ranks_)
+            log_msg(LogLevel::Info, R.topo.describe(), " backend cpu threads ",
+                    cfg_.threads > 0 ? cfg_.threads : omp_get_max_threads());
     }
 
     // ---- compute ---------------------------------------------------------------------

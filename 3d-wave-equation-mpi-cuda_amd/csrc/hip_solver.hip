@@ -21,7 +21,10 @@
 #include "checkpoint.hpp"
 #include "hip_kernels.hpp"
 #include "problem.hpp"
+#include "sizing.hpp"
 #include "solver.hpp"
+#include "log.hpp"
+#include "trace.hpp"
 
 #define HIP_CHECK(x)                                                                   \
     do {                                                                               \
@@ -37,22 +40,6 @@ namespace {
 using clk = std::chrono::steady_clock;
 
 // Temporal-blocking variant names: "tb2" (2 rows/lane, 4 waves), "tb2r<R>", "tb2r<R>w<W>".
-void parse_tb_name(const std::string& name, int& rows, int& waves) {
-    rows = 2, waves = 4;
-    std::string s = name.substr(3);
-    if (!s.empty() && s[0] == 'r') {
-        size_t n = 0;
-        rows = std::stoi(s.substr(1), &n);
-        s = s.substr(1 + n);
-    }
-    if (!s.empty() && s[0] == 'w') {
-        size_t n = 0;
-        waves = std::stoi(s.substr(1), &n);
-        s = s.substr(1 + n);
-    }
-    W3D_REQUIRE(s.empty() && tb2_supported(rows, waves), "wave3d: unknown kernel variant " + name);
-}
-
 std::string tb_name(int rows, int waves) {
     std::string s = rows == 2 && waves == 4 ? "tb2" : "tb2r" + std::to_string(rows);
     if (waves != 4) s += "w" + std::to_string(waves);
@@ -108,22 +95,18 @@ public:
             world_ = std::max(1, c.ranks);
             for (int r = 0; r < world_; ++r) local_.push_back(r);
         }
-        // "auto": temporal blocking (tb2, chunk 96, measured fastest on MI355X, profiles/) whenever the
-        // decomposition allows it (one rank, or x slabs); otherwise the single-step march2.
-        const bool yz_split = (c.dims[1] > 1 || c.dims[2] > 1);
-        const bool auto_tb = c.kernel == "auto" && !yz_split;
-        tb_ = auto_tb || c.kernel.rfind("tb2", 0) == 0;
-        if (auto_tb) tb_rows_ = 2, tb_waves_ = 4;
-        else if (tb_) parse_tb_name(c.kernel, tb_rows_, tb_waves_);
+        // kernel family, ghost depth, levels and decomposition (sizing.cpp: shared with the
+        // --fill-hbm planner, so a planned N is exactly what gets allocated)
+        const Layout lay = plan_layout(c, world_);
+        tb_ = lay.tb;
+        tb_rows_ = lay.rows;
+        tb_waves_ = lay.waves;
+        G_ = lay.G;
+        L_ = lay.L;
+        for (int a = 0; a < 3; ++a) cfg_.dims[a] = lay.dims[a];
+        W3D_REQUIRE(!tb_ || tb2_supported(tb_rows_, tb_waves_), "wave3d: unknown kernel variant " + c.kernel);
         kind_ = parse_kernel_variant(tb_ ? std::string("auto") : c.kernel);
         naive_.march = false;
-        G_ = tb_ ? 2 : 1;
-        L_ = tb_ ? 4 : 3;
-        // temporal blocking across ranks: 2-deep x halos, so the decomposition is x slabs
-        if (tb_ && world_ > 1 && !(c.dims[0] || c.dims[1] || c.dims[2])) {
-            cfg_.dims[0] = world_;
-            cfg_.dims[1] = cfg_.dims[2] = 1;
-        }
         // interior/shell split + comm stream whenever there is a remote halo to hide
         overlap_ = c.overlap && (ext_ != nullptr || world_ > 1);
     }
@@ -131,10 +114,25 @@ public:
     ~HipSolver() { release(); }
 
     void init() {
+        TraceRange tr("wave3d.setup");
         auto t0 = clk::now();
         setup();
         HIP_CHECK(hipDeviceSynchronize());
         init_ms_ = std::chrono::duration<double, std::milli>(clk::now() - t0).count();
+        if (log_on(LogLevel::Info)) {
+            for (auto& R : ranks_) {
+                log_msg(LogLevel::Info, R.topo.describe(), " kernel ",
+                        tb_ ? tb_name(tb_rows_, tb_waves_) : kernel_variant_name(kind_), " levels ",
+                        L_, " ghost ", G_, " bytes/level ", R.elems * sizeof(T), " overlap ",
+                        overlap_ ? "on" : "off", " transport ",
+                        ext_ ? ext_->name() : (world_ > 1 ? "loopback" : "self"));
+                log_msg(LogLevel::Debug, "rank ", R.topo.rank, ": ", R.plan.sends.size(),
+                        " face sends, ", R.tb_sends.size(), " deep-halo sends, interior ",
+                        R.interior.empty() ? 0 : 1, " shell boxes ", R.shell.size(), "/",
+                        R.tb_shell.size());
+            }
+            log_msg(LogLevel::Info, "setup ", init_ms_, " ms");
+        }
     }
 
     double init_ms() const { return init_ms_; }
@@ -535,6 +533,7 @@ private:
 
     // ---- time loop --------------------------------------------------------------------
     void solve(RunResult& res, Timings& tm) {
+        TraceRange tr("wave3d.solve");
         const int K = prob_.K;
         for (auto e : prof_) (void)hipEventDestroy(e);
         prof_.clear();
@@ -567,6 +566,7 @@ private:
         res.graph = gexec_ != nullptr;
 
         // final max-reduction of the per-layer slots (mpi_new.cpp:358-361)
+        TraceRange trr("wave3d.reduce");
         prof_mark(s_comp_, 4);
         const size_t nslot = size_t(K + 1) * kSlotsPerLayer;
         std::vector<u64> acc(nslot, 0);
@@ -601,6 +601,7 @@ private:
 
     // ---- time loop ----------------------------------------------------------------------
     void enqueue_ic() {
+        TraceRange tr("wave3d.ic");
         prof_mark(s_comp_, 0);
         for (auto& R : ranks_) {
             launch_init<T>(R.g[0], R.gv, R.owned, tb_ ? R.wrap2 : R.wrap, R.tx, R.ty, R.tz, ct_[0],
@@ -614,11 +615,14 @@ private:
     // Layers start..K on the streams; host work only for --check-every / checkpoints.
     // Returns the last layer computed.
     int enqueue_layers(RunResult& res, int start) {
+        TraceRange tr("wave3d.layers");
         const int K = prob_.K;
         int done = start - 1;
         for (int n = start; n <= K;) {
             // temporal blocking: layers n and n+1 in one sweep; a lone last layer single-step
             const int span = (tb_ && n + 1 <= K) ? 2 : 1;
+            if (cfg_.print_layers && !cfg_.quiet && ranks_[0].topo.rank == 0)
+                for (int q = n; q < n + span; ++q) std::cout << "calculating layer " << q << "\n";
             prof_mark(s_comp_, 0);
             for (int q = n; q < n + span; ++q)
                 for (auto& R : ranks_)
@@ -670,10 +674,12 @@ private:
     // faults); a failed capture falls back to direct launches.
     bool graph_eligible() const {
         return cfg_.graph != 0 && !ext_ && cfg_.check_every == 0 && cfg_.checkpoint_every == 0 &&
-               cfg_.resume_dir.empty() && !cfg_.profile && fault_.kind.empty();
+               cfg_.resume_dir.empty() && !cfg_.profile && fault_.kind.empty() &&
+               !cfg_.print_layers;
     }
 
     void build_graph(RunResult& res) {
+        TraceRange tr("wave3d.graph_capture");
         hipGraph_t g = nullptr;
         try {
             HIP_CHECK(hipStreamBeginCapture(s_comp_, hipStreamCaptureModeThreadLocal));
@@ -682,6 +688,7 @@ private:
             HIP_CHECK(hipStreamEndCapture(s_comp_, &g));
             HIP_CHECK(hipGraphInstantiate(&gexec_, g, nullptr, nullptr, 0));
             HIP_CHECK(hipGraphDestroy(g));
+            log_msg(LogLevel::Info, "captured IC + ", prob_.K, " layers as one hipGraph");
         } catch (const Error& e) {
             hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
             if (hipStreamIsCapturing(s_comp_, &st) == hipSuccess && st != hipStreamCaptureStatusNone) {
@@ -694,8 +701,9 @@ private:
             gexec_ = nullptr;
             graph_failed_ = true;
             if (cfg_.graph == 1) throw;
-            if (!cfg_.quiet) std::cerr << "wave3d: hipGraph capture failed (" << e.what()
-                                       << "), using direct launches\n";
+            if (!cfg_.quiet)
+                log_msg(LogLevel::Warn, "hipGraph capture failed (", e.what(),
+                        "), using direct launches");
         }
     }
 
@@ -815,6 +823,8 @@ private:
             CheckpointHeader h = make_header(cfg_, R.topo, n, sizeof(T));
             write_checkpoint(cfg_.checkpoint_dir, h, host_level(R, prev, lp), host_level(R, cur, lc),
                              a, r);
+            log_msg(LogLevel::Info, "rank ", R.topo.rank, ": checkpoint after layer ", n, " -> ",
+                    checkpoint_path(cfg_.checkpoint_dir, R.topo.rank));
         }
     }
 

@@ -14,6 +14,7 @@
 
 #include "cli_common.hpp"
 #include "rccl_transport.hpp"
+#include "sizing.hpp"
 #include "solver.hpp"
 
 using namespace wave3d;
@@ -26,13 +27,27 @@ static int env_int(const char* k, int dflt) {
 int main(int argc, char** argv) {
     try {
         Config c = parse_cli(argc, argv);
-        Problem p = Problem::from_config(c);
         int ndev = 0;
         if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) {
             std::cerr << "wave3d: no HIP device found (use wave3d_cpu for the OpenMP backend)\n";
             return 1;
         }
         const int world = env_int("WORLD_SIZE", 1);
+        if (c.fill_hbm > 0) {
+            // size the grid to the device: every rank of the job has the
+            // same HBM; simulated ranks share one device
+            const int dev = c.device >= 0 ? c.device : (world > 1 ? env_int("LOCAL_RANK", 0) % ndev : 0);
+            size_t freeb = 0, total = 0;
+            if (hipSetDevice(dev) != hipSuccess || hipMemGetInfo(&freeb, &total) != hipSuccess)
+                throw Error("hipMemGetInfo failed");
+            const int nr = world > 1 ? world : (c.Np > 1 && c.ranks == 0 ? c.Np : std::max(1, c.ranks));
+            const double budget = c.fill_hbm * double(total) / (world > 1 || c.ranks == 0 ? 1 : c.ranks);
+            c.N = fill_hbm_N(c, nr, budget);
+            if (!c.quiet && env_int("RANK", 0) == 0)
+                std::cout << "fill-hbm: N = " << c.N << " (" << device_bytes_per_rank(c, nr) / 1e9
+                          << " GB per GPU of " << total / 1e9 << " GB)" << std::endl;
+        }
+        Problem p = Problem::from_config(c);
         if (world > 1) {
             const int rank = env_int("RANK", 0);
             const int local = env_int("LOCAL_RANK", rank);

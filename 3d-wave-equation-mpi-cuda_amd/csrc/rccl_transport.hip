@@ -1,4 +1,5 @@
 #include "rccl_transport.hpp"
+#include "trace.hpp"
 
 #include <arpa/inet.h>
 #include <hip/hip_runtime.h>
@@ -63,6 +64,7 @@ RcclTransport::~RcclTransport() {
 
 void RcclTransport::exchange(const std::vector<Message>& sends, const std::vector<Message>& recvs,
                              void* stream) {
+    TraceRange tr("rccl.exchange");
     hipStream_t s = static_cast<hipStream_t>(stream);
     NCCL_CHECK(ncclGroupStart());
     for (const auto& m : sends)

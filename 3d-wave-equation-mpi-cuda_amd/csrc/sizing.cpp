@@ -1,0 +1,84 @@
+#include "sizing.hpp"
+
+#include <algorithm>
+
+#include "common.hpp"
+#include "topology.hpp"
+
+namespace wave3d {
+
+static void parse_tb(const std::string& name, int& rows, int& waves) {
+    rows = 2, waves = 4;
+    std::string s = name.substr(3);
+    if (!s.empty() && s[0] == 'r') {
+        size_t n = 0;
+        rows = std::stoi(s.substr(1), &n);
+        s = s.substr(1 + n);
+    }
+    if (!s.empty() && s[0] == 'w') {
+        size_t n = 0;
+        waves = std::stoi(s.substr(1), &n);
+        s = s.substr(1 + n);
+    }
+    W3D_REQUIRE(s.empty(), "wave3d: unknown kernel variant " + name);
+}
+
+Layout plan_layout(const Config& c, int world) {
+    Layout l;
+    // "auto": temporal blocking (tb2, measured fastest on MI355X, profiles/) whenever the
+    // decomposition allows it (one rank, or x slabs); otherwise the single-step march2.
+    const bool yz_split = c.dims[1] > 1 || c.dims[2] > 1;
+    const bool auto_tb = c.kernel == "auto" && !yz_split;
+    l.tb = auto_tb || c.kernel.rfind("tb2", 0) == 0;
+    if (l.tb && !auto_tb) parse_tb(c.kernel, l.rows, l.waves);
+    l.G = l.tb ? 2 : 1;
+    l.L = l.tb ? 4 : 3;
+    for (int a = 0; a < 3; ++a) l.dims[a] = c.dims[a];
+    // temporal blocking across ranks: 2-deep x halos, so the decomposition is x slabs
+    if (l.tb && world > 1 && !(c.dims[0] || c.dims[1] || c.dims[2])) {
+        l.dims[0] = world;
+        l.dims[1] = l.dims[2] = 1;
+    }
+    return l;
+}
+
+size_t level_elems(int X, int Y, int Z, int G, int elem_size) {
+    const int A = 128 / elem_size;  // rows start on a 128-B boundary
+    const size_t sj = size_t((A + Z + G + A - 1) / A) * A;
+    return size_t(X + 2 * G) * size_t(Y + 2 * G) * sj;
+}
+
+size_t device_bytes_per_rank(const Config& c, int world) {
+    const Layout l = plan_layout(c, world);
+    const int es = c.dtype == DType::F64 ? 8 : 4;
+    const bool have = l.dims[0] || l.dims[1] || l.dims[2];
+    size_t best = 0;
+    // extents differ only for the last coordinate on an axis: the last rank is the largest
+    const Topology t = Topology::make(c.N, world, world - 1, have ? l.dims : nullptr);
+    const int X = t.X(), Y = t.Y(), Z = t.Z();
+    best = size_t(l.L) * level_elems(X, Y, Z, l.G, es) * es;
+    best += size_t(X + Y + Z + 6) * es;                   // analytic tables
+    best += size_t(c.timesteps + 1) * 3 * 8;              // error slots
+    best += 2 * size_t(std::max(X, 1)) * (std::max(Y, Z) + 2) * es * 4;  // y/z face buffers
+    if (l.tb && world > 1) best += size_t(Y + 2 * l.G) * (Z + 2 * l.G + 32) * es;  // seam plane
+    return best;
+}
+
+int fill_hbm_N(const Config& c, int world, double budget_bytes) {
+    Config q = c;
+    int lo = 8, hi = 8;
+    auto fits = [&](int N) {
+        q.N = N;
+        return double(device_bytes_per_rank(q, world)) <= budget_bytes;
+    };
+    W3D_REQUIRE(fits(lo), "fill-hbm: not even N=8 fits the budget");
+    while (fits(hi * 2)) hi *= 2;
+    lo = hi, hi = hi * 2;  // fits(lo), !fits(hi)
+    while (hi - lo > 1) {
+        const int mid = lo + (hi - lo) / 2;
+        (fits(mid) ? lo : hi) = mid;
+    }
+    return lo;
+}
+
+}  // namespace wave3d

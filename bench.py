@@ -36,7 +36,10 @@ def main() -> int:
     ap.add_argument("--steps", type=int, default=5, help="timed solves")
     ap.add_argument("--warmup", type=int, default=2, help="untimed solves")
     ap.add_argument("--N", type=int, default=0, help="override global N (default: weak scaling from 512)")
-    ap.add_argument("--timesteps", type=int, default=100)
+    ap.add_argument("--timesteps", type=int, default=100,
+                    help="layers per solve (0: smallest stable count with margin, C <= 0.5)")
+    ap.add_argument("--fill-hbm", type=float, default=0.0,
+                    help="size N to this fraction of each GPU's HBM (SURVEY §7.3; e.g. 0.9)")
     ap.add_argument("--dtype", default="fp64", choices=["fp64", "fp32"])
     ap.add_argument("--kernel", default="auto")
     ap.add_argument("--chunk", type=int, default=0)
@@ -79,6 +82,19 @@ def main() -> int:
         torch.cuda.set_device(0)
 
     N = a.N or presets.weak_scaling_N(n_gpus)
+    if a.fill_hbm > 0:
+        if a.backend != "hip":
+            print("bench: --fill-hbm needs the hip backend", file=sys.stderr)
+            return 2
+        total = torch.cuda.mem_get_info()[1]
+        probe = wave3d.WaveSolver(wave3d.WaveProblem(N, timesteps=max(1, a.timesteps), dtype=a.dtype),
+                                  a.backend, Np=n_gpus, kernel=a.kernel).args()
+        N = C.fill_hbm_N(probe, n_gpus, a.fill_hbm * total)
+    K = a.timesteps
+    if K <= 0:
+        K = wave3d.WaveProblem(N, dtype=a.dtype).min_stable_timesteps()
+        K = max(20, int(K * 0.577 / 0.5) + 1)  # C <= 0.5
+    a.timesteps = K
     prob = wave3d.WaveProblem(N, timesteps=a.timesteps, dtype=a.dtype)
     if not prob.stable():
         print(f"bench: warning: C={prob.courant:.3f} > 1/sqrt(3) (unstable)", file=sys.stderr)
@@ -137,6 +153,9 @@ def main() -> int:
             "kernel": res["kernel"],
             "overlap": not a.no_overlap,
             "hip_graph": bool(res.get("graph", False)),
+            "fill_hbm": a.fill_hbm or None,
+            "device_bytes_per_gpu": C.memory_plan(args, n_gpus)["bytes_per_rank"]
+                                     if a.backend == "hip" else None,
         },
         "linf_abs": res["linf_abs"],
         "linf_final_layer": res["timesteps"],

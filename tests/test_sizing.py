@@ -1,0 +1,68 @@
+"""Device-memory planning (sizing.cpp) and small CLI knobs
+(--graph, --fill-hbm, WAVE_LOG levels)."""
+import os
+import subprocess
+
+import pytest
+
+ARGS = ["512", "1", "pi", "pi", "pi", "1", "100"]
+
+
+def test_layout_auto_is_temporal_blocking_on_slabs(C):
+    p1 = C.memory_plan(ARGS, 1)
+    assert p1["tb"] and p1["ghost"] == 2 and p1["levels"] == 4
+    p8 = C.memory_plan(ARGS, 8)
+    assert p8["tb"] and p8["dims"] == [8, 1, 1]
+    m = C.memory_plan(ARGS + ["--kernel", "march2"], 8)
+    assert not m["tb"] and m["ghost"] == 1 and m["levels"] == 3 and m["dims"] == [0, 0, 0]
+    y = C.memory_plan(ARGS + ["--dims", "2,2,2"], 8)  # y/z split: single-step kernel
+    assert not y["tb"]
+
+
+def test_bytes_per_rank_matches_level_formula(C):
+    # one rank, N=512 fp64, temporal blocking: 4 levels of (513+4)^2 x roundup(16+513+2, 16)
+    sj = ((16 + 513 + 2 + 15) // 16) * 16
+    level = (513 + 4) * (513 + 4) * sj * 8
+    b = C.memory_plan(ARGS, 1)["bytes_per_rank"]
+    assert 4 * level <= b < 4 * level * 1.01
+    # fp32 halves the levels; 8 slabs divide them by ~8
+    b32 = C.memory_plan(ARGS + ["--dtype", "fp32"], 1)["bytes_per_rank"]
+    assert 0.45 * b < b32 < 0.55 * b
+    assert C.memory_plan(ARGS, 8)["bytes_per_rank"] < b / 7
+
+
+@pytest.mark.parametrize("extra,world", [([], 1), (["--dtype", "fp32"], 8),
+                                         (["--kernel", "march2", "--dims", "2,2,2"], 8)])
+def test_fill_hbm_is_tight(C, extra, world):
+    budget = 0.9 * 288e9
+    N = C.fill_hbm_N(ARGS + extra, world, budget)
+    at = lambda n: C.memory_plan([str(n)] + ARGS[1:] + extra, world)["bytes_per_rank"]
+    assert at(N) <= budget < at(N + 1)
+    assert N > 1900  # 288 GB per GPU holds ~2000^3 fp64 nodes with 4 levels
+
+
+def test_fill_hbm_survey_estimate(C):
+    # 3 fp64 levels per GPU on 2x2x2 -> ~4,400^3 global
+    N = C.fill_hbm_N(ARGS + ["--kernel", "march2", "--dims", "2,2,2"], 8, 0.9 * 288e9)
+    assert 4300 <= N <= 4500
+
+
+def test_cli_graph_and_fill_flags(C):
+    C.parse(ARGS + ["--graph", "off"])
+    C.parse(ARGS + ["--fill-hbm", "0.9"])
+    with pytest.raises(Exception):
+        C.parse(ARGS + ["--graph", "sometimes"])
+    with pytest.raises(Exception):
+        C.parse(ARGS + ["--fill-hbm", "1.5"])
+
+
+def test_wave_log_levels(cpu_prog):
+    env = dict(os.environ, WAVE_LOG="info")
+    r = subprocess.run([cpu_prog, "12", "1", "pi", "pi", "pi", "1", "3", "--format", "none",
+                        "--ranks", "2", "--quiet"], env=env, capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0
+    assert "wave3d[info] rank 0/2 dims 2x1x1" in r.stderr
+    env["WAVE_LOG"] = "warn"
+    r = subprocess.run([cpu_prog, "12", "1", "pi", "pi", "pi", "1", "3", "--format", "none",
+                        "--quiet"], env=env, capture_output=True, text=True, timeout=60)
+    assert "wave3d[info]" not in r.stderr
