@@ -402,6 +402,29 @@ __global__ void k_encode(const double* v, u64* k, int n) {
     if (t < n) k[t] = enc_key(v[t]);
 }
 
+template <class T>
+struct BoxCopyOps {
+    BoxCopy<T> op[kMaxBoxCopy];
+};
+
+template <class T>
+__global__ void __launch_bounds__(kThreads) k_box_copy(const BoxCopyOps<T> ops, i64 si, int sj,
+                                                       bool to_buf) {
+    const BoxCopy<T> o = ops.op[blockIdx.y];
+    const int nk = o.b.k1 - o.b.k0 + 1, nj = o.b.j1 - o.b.j0 + 1;
+    const i64 total = i64(o.b.i1 - o.b.i0 + 1) * nj * nk;
+    for (i64 e = i64(blockIdx.x) * blockDim.x + threadIdx.x; e < total;
+         e += i64(gridDim.x) * blockDim.x) {
+        const int k = o.b.k0 + int(e % nk);
+        const i64 r = e / nk;
+        const int j = o.b.j0 + int(r % nj);
+        const int i = o.b.i0 + int(r / nj);
+        T* g = o.grid + i64(i) * si + i64(j) * sj + k;
+        if (to_buf) o.buf[e] = *g;
+        else *g = o.buf[e];
+    }
+}
+
 }  // namespace
 
 int march_rows_per_thread() { return 4; }
@@ -609,5 +632,29 @@ void launch_encode_keys(const double* v, u64* k, int n, hipStream_t s) {
     template void launch_faces<T>(T*, const GridView&, const FaceOp<T>*, int, bool, hipStream_t);
 W3D_INST(double)
 W3D_INST(float)
+
+
+template <class T>
+void launch_box_copy(const BoxCopy<T>* ops, int nops, const GridView& gv, bool to_buf,
+                     hipStream_t s) {
+    W3D_REQUIRE(nops >= 0 && nops <= kMaxBoxCopy, "too many halo boxes in one launch");
+    if (nops == 0) return;
+    BoxCopyOps<T> p{};
+    i64 most = 0;
+    for (int q = 0; q < nops; ++q) {
+        const Box& b = ops[q].b;
+        W3D_REQUIRE(!b.empty() && b.i0 >= 1 - gv.G && b.i1 <= gv.X + gv.G && b.j0 >= 1 - gv.G &&
+                        b.j1 <= gv.Y + gv.G && b.k0 >= 1 - gv.G && b.k1 <= gv.Z + gv.G,
+                    "halo box outside the storage");
+        p.op[q] = ops[q];
+        most = std::max(most, i64(b.i1 - b.i0 + 1) * (b.j1 - b.j0 + 1) * (b.k1 - b.k0 + 1));
+    }
+    const int blocks = int(std::min<i64>(2048, (most + kThreads - 1) / kThreads));
+    hipLaunchKernelGGL(k_box_copy<T>, dim3(blocks, nops), dim3(kThreads), 0, s, p, gv.si, gv.sj,
+                       to_buf);
+    HIP_OK(hipGetLastError());
+}
+template void launch_box_copy<double>(const BoxCopy<double>*, int, const GridView&, bool, hipStream_t);
+template void launch_box_copy<float>(const BoxCopy<float>*, int, const GridView&, bool, hipStream_t);
 
 }  // namespace wave3d

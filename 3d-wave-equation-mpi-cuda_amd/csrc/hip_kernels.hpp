@@ -95,6 +95,20 @@ template <class T>
 void launch_faces(T* u, const GridView& gv, const FaceOp<T>* ops, int nops, bool to_buf,
                   hipStream_t s);
 
+// Box halo staging for the temporal-blocking exchange on y/z splits: copy the logical box
+// `b` of a level (origin `grid` = logical (0,0,0), strides of `gv`) to / from a contiguous
+// buffer (k fastest). Up to kMaxBoxCopy boxes per launch.
+constexpr int kMaxBoxCopy = 8;
+template <class T>
+struct BoxCopy {
+    T* grid = nullptr;
+    T* buf = nullptr;
+    Box b;
+};
+template <class T>
+void launch_box_copy(const BoxCopy<T>* ops, int nops, const GridView& gv, bool to_buf,
+                     hipStream_t s);
+
 // Initialise per-layer error slots: abs/rel keys = encode(-100), flag = 0.
 void launch_init_err(u64* err, int layers, hipStream_t s);
 

@@ -74,6 +74,16 @@ struct DevRank {
         int nplanes;
     };
     std::vector<PlaneMsg> tb_sends, tb_recvs;
+    // y/z splits: rows / columns of depth 2 (D) and 1 (C), staged through buffers; round 0
+    // (y) and round 1 (z) run after the x planes, each over the full extent of the previous
+    // axes (ghosts included), so edges arrive without diagonal messages
+    struct BoxMsg {
+        int peer, tag;
+        int level;      // 0 = D level, 1 = C level
+        Box box;
+        T* buf;
+    };
+    std::vector<BoxMsg> tb_bsends[2], tb_brecvs[2];
     T* alias_buf = nullptr;      // one plane: x=N (first x-rank) or x=0 (last x-rank)
     Box tb_interior;
     std::vector<Box> tb_shell;
@@ -288,6 +298,10 @@ private:
             for (auto* p : R.rbuf) (void)hipFree(p);
             (void)hipFree(R.err);
             (void)hipFree(R.alias_buf);
+            for (int q = 0; q < 2; ++q) {
+                for (auto& m : R.tb_bsends[q]) (void)hipFree(m.buf);
+                for (auto& m : R.tb_brecvs[q]) (void)hipFree(m.buf);
+            }
         }
         ranks_.clear();
         if (s_comp_) (void)hipStreamDestroy(s_comp_);
@@ -352,46 +366,91 @@ private:
         R.tb_sends.clear();
         R.tb_recvs.clear();
         const auto& t = R.topo;
-        const int X = t.X();
+        const int X = t.X(), Y = t.Y(), Z = t.Z();
         R.tb_interior = R.compute;
         R.tb_shell.clear();
-        if (!tb_ || R.plan.self_x) return;
-        W3D_REQUIRE(t.dims[1] == 1 && t.dims[2] == 1,
-                    "temporal blocking across ranks needs an x-slab decomposition (--dims P,1,1)");
-        W3D_REQUIRE(X >= 4, "temporal blocking needs >= 4 x planes per rank");
-        const bool first = t.first(0), last = t.last(0);
-        const int up = t.nbr[0][1], dn = t.nbr[0][0];
+        const bool ysplit = t.dims[1] > 1, zsplit = t.dims[2] > 1;
+        if (!tb_ || (R.plan.self_x && !ysplit && !zsplit)) return;
         using M = typename DevRank<T>::PlaneMsg;
-        R.tb_sends.push_back(M{up, 11, 0, last ? X - 2 : X - 1, 2});
-        if (last) R.tb_sends.push_back(M{up, 12, 0, X, 1});
-        R.tb_sends.push_back(M{up, 13, 1, t.x_send_plus(), 1});
-        R.tb_sends.push_back(M{dn, 21, 0, first ? 2 : 1, 2});
-        if (first) R.tb_sends.push_back(M{dn, 22, 0, 1, 1});
-        R.tb_sends.push_back(M{dn, 23, 1, t.x_send_minus(), 1});
-        R.tb_recvs.push_back(M{dn, 11, 0, -1, 2});
-        if (first) R.tb_recvs.push_back(M{dn, 12, 0, kAliasPlane, 1});
-        R.tb_recvs.push_back(M{dn, 13, 1, 0, 1});
-        R.tb_recvs.push_back(M{up, 21, 0, X + 1, 2});
-        if (last) R.tb_recvs.push_back(M{up, 22, 0, kAliasPlane, 1});
-        R.tb_recvs.push_back(M{up, 23, 1, X + 1, 1});
-        if (first || last) {
-            HIP_CHECK(hipMalloc(&R.alias_buf, R.gv.si * sizeof(T)));
-            HIP_CHECK(hipMemset(R.alias_buf, 0, R.gv.si * sizeof(T)));
+        using BM = typename DevRank<T>::BoxMsg;
+        // ---- x: whole planes (contiguous, sent in place) ----------------------------------
+        if (!R.plan.self_x) {
+            W3D_REQUIRE(X >= 4, "temporal blocking needs >= 4 x planes per rank");
+            const bool first = t.first(0), last = t.last(0);
+            const int up = t.nbr[0][1], dn = t.nbr[0][0];
+            R.tb_sends.push_back(M{up, 11, 0, last ? X - 2 : X - 1, 2});
+            if (last) R.tb_sends.push_back(M{up, 12, 0, X, 1});
+            R.tb_sends.push_back(M{up, 13, 1, t.x_send_plus(), 1});
+            R.tb_sends.push_back(M{dn, 21, 0, first ? 2 : 1, 2});
+            if (first) R.tb_sends.push_back(M{dn, 22, 0, 1, 1});
+            R.tb_sends.push_back(M{dn, 23, 1, t.x_send_minus(), 1});
+            R.tb_recvs.push_back(M{dn, 11, 0, -1, 2});
+            if (first) R.tb_recvs.push_back(M{dn, 12, 0, kAliasPlane, 1});
+            R.tb_recvs.push_back(M{dn, 13, 1, 0, 1});
+            R.tb_recvs.push_back(M{up, 21, 0, X + 1, 2});
+            if (last) R.tb_recvs.push_back(M{up, 22, 0, kAliasPlane, 1});
+            R.tb_recvs.push_back(M{up, 23, 1, X + 1, 1});
+            if (first || last) {
+                HIP_CHECK(hipMalloc(&R.alias_buf, R.gv.si * sizeof(T)));
+                HIP_CHECK(hipMemset(R.alias_buf, 0, R.gv.si * sizeof(T)));
+            }
         }
-        // D on planes 1,2 / X-1,X depends on received ghosts (through C on 0,1 / X,X+1)
-        Box in = R.compute;
-        in.i0 = std::max(in.i0, 3);
-        in.i1 = std::min(in.i1, X - 2);
+        // ---- y (round 0) and z (round 1): D depth 2, C depth 1 ----------------------------
+        const int G = G_;
+        for (int ax = 1; ax <= 2; ++ax) {
+            if (t.dims[ax] == 1) continue;
+            const int n = ax == 1 ? Y : Z;
+            W3D_REQUIRE(n >= 4, "temporal blocking needs >= 4 nodes per rank on split axes");
+            auto box = [&](int lo, int hi) {
+                // full extent (ghosts included) on the axes exchanged before this one
+                Box b{1 - G, X + G, 1, Y, 1, Z};
+                if (ax == 1) b.j0 = lo, b.j1 = hi;
+                else b.j0 = 1 - G, b.j1 = Y + G, b.k0 = lo, b.k1 = hi;
+                return b;
+            };
+            auto add = [&](std::vector<BM>& v, int peer, int tag, int level, Box b) {
+                const size_t cnt = size_t(b.i1 - b.i0 + 1) * (b.j1 - b.j0 + 1) * (b.k1 - b.k0 + 1);
+                T* buf = nullptr;
+                HIP_CHECK(hipMalloc(&buf, cnt * sizeof(T)));
+                v.push_back(BM{peer, tag, level, b, buf});
+            };
+            const int base = ax == 1 ? 30 : 50;
+            const int dn = t.nbr[ax][0], up = t.nbr[ax][1];
+            auto& S = R.tb_bsends[ax - 1];
+            auto& V = R.tb_brecvs[ax - 1];
+            // sends: down (to dn) then up; receives: from down then from up — the same
+            // per-peer order on both sides (tag-less RCCL matching)
+            if (dn >= 0) add(S, dn, base + 1, 0, box(1, 2)), add(S, dn, base + 2, 1, box(1, 1));
+            if (up >= 0) add(S, up, base + 11, 0, box(n - 1, n)), add(S, up, base + 12, 1, box(n, n));
+            if (dn >= 0) add(V, dn, base + 11, 0, box(-1, 0)), add(V, dn, base + 12, 1, box(0, 0));
+            if (up >= 0) add(V, up, base + 1, 0, box(n + 1, n + 2)), add(V, up, base + 2, 1, box(n + 1, n + 1));
+        }
+        // D within 2 nodes of a received ghost depends on it (through C on the ring)
+        Box c = R.compute, in = c;
+        if (!R.plan.self_x) in.i0 = std::max(in.i0, 3), in.i1 = std::min(in.i1, X - 2);
+        if (t.nbr[1][0] >= 0) in.j0 = std::max(in.j0, 3);
+        if (t.nbr[1][1] >= 0) in.j1 = std::min(in.j1, Y - 2);
+        if (t.nbr[2][0] >= 0) in.k0 = std::max(in.k0, 3);
+        if (t.nbr[2][1] >= 0) in.k1 = std::min(in.k1, Z - 2);
         R.tb_interior = in;
-        if (in.empty()) {
-            R.tb_shell.push_back(R.compute);
-        } else {
-            Box a = R.compute, b = R.compute;
-            a.i1 = in.i0 - 1;
-            b.i0 = in.i1 + 1;
-            if (!a.empty()) R.tb_shell.push_back(a);
+        auto add = [&](Box b) {
             if (!b.empty()) R.tb_shell.push_back(b);
+        };
+        if (in.empty()) {
+            add(c);
+        } else {
+            add({c.i0, in.i0 - 1, c.j0, c.j1, c.k0, c.k1});
+            add({in.i1 + 1, c.i1, c.j0, c.j1, c.k0, c.k1});
+            add({in.i0, in.i1, c.j0, in.j0 - 1, c.k0, c.k1});
+            add({in.i0, in.i1, in.j1 + 1, c.j1, c.k0, c.k1});
+            add({in.i0, in.i1, in.j0, in.j1, c.k0, in.k0 - 1});
+            add({in.i0, in.i1, in.j0, in.j1, in.k1 + 1, c.k1});
         }
+    }
+
+    bool tb_halo(const DevRank<T>& R) const {
+        return !R.tb_sends.empty() || !R.tb_bsends[0].empty() || !R.tb_bsends[1].empty() ||
+               !R.tb_brecvs[0].empty() || !R.tb_brecvs[1].empty();
     }
 
     void* tb_ptr(DevRank<T>& R, const typename DevRank<T>::PlaneMsg& m, int mD) {
@@ -408,7 +467,7 @@ private:
                 snd.push_back({m.peer, m.tag, tb_ptr(R, m, mD), size_t(m.nplanes) * R.gv.si * sizeof(T)});
             for (auto& m : R.tb_recvs)
                 rcv.push_back({m.peer, m.tag, tb_ptr(R, m, mD), size_t(m.nplanes) * R.gv.si * sizeof(T)});
-            ext_->exchange(snd, rcv, s);
+            if (!snd.empty() || !rcv.empty()) ext_->exchange(snd, rcv, s);
         } else {
             for (auto& S : ranks_)
                 for (auto& m : S.tb_sends) {
@@ -425,6 +484,56 @@ private:
                         }
                     W3D_REQUIRE(done, "unmatched tb halo message");
                 }
+        }
+        // y then z rounds: pack -> transport / D2D -> unpack, strictly after the x planes
+        for (int rd = 0; rd < 2; ++rd) {
+            bool any = false;
+            for (auto& R : ranks_) any |= !R.tb_bsends[rd].empty() || !R.tb_brecvs[rd].empty();
+            if (!any) continue;
+            auto ops = [&](DevRank<T>& R, std::vector<typename DevRank<T>::BoxMsg>& v) {
+                std::vector<BoxCopy<T>> o;
+                for (auto& m : v) {
+                    BoxCopy<T> b;
+                    b.grid = R.g[lvl(m.level == 0 ? mD : mD - 1 + L_)];
+                    b.buf = m.buf;
+                    b.b = m.box;
+                    o.push_back(b);
+                }
+                return o;
+            };
+            for (auto& R : ranks_) {
+                auto o = ops(R, R.tb_bsends[rd]);
+                launch_box_copy<T>(o.data(), int(o.size()), R.gv, true, s);
+            }
+            auto bytes = [](const typename DevRank<T>::BoxMsg& m) {
+                const Box& b = m.box;
+                return size_t(b.i1 - b.i0 + 1) * (b.j1 - b.j0 + 1) * (b.k1 - b.k0 + 1) * sizeof(T);
+            };
+            if (ext_) {
+                auto& R = ranks_[0];
+                std::vector<Message> snd, rcv;
+                for (auto& m : R.tb_bsends[rd]) snd.push_back({m.peer, m.tag, m.buf, bytes(m)});
+                for (auto& m : R.tb_brecvs[rd]) rcv.push_back({m.peer, m.tag, m.buf, bytes(m)});
+                ext_->exchange(snd, rcv, s);
+            } else {
+                for (auto& S : ranks_)
+                    for (auto& m : S.tb_bsends[rd]) {
+                        bool done = false;
+                        for (auto& g : ranks_[m.peer].tb_brecvs[rd])
+                            if (g.peer == S.topo.rank && g.tag == m.tag) {
+                                W3D_REQUIRE(bytes(g) == bytes(m), "tb box halo size mismatch");
+                                HIP_CHECK(hipMemcpyAsync(g.buf, m.buf, bytes(m),
+                                                         hipMemcpyDeviceToDevice, s));
+                                done = true;
+                                break;
+                            }
+                        W3D_REQUIRE(done, "unmatched tb box halo message");
+                    }
+            }
+            for (auto& R : ranks_) {
+                auto o = ops(R, R.tb_brecvs[rd]);
+                launch_box_copy<T>(o.data(), int(o.size()), R.gv, false, s);
+            }
         }
         for (auto& R : ranks_) inject_after_exchange(R, mD, s);
     }
@@ -709,7 +818,7 @@ private:
 
     // exchange of layer n: overlapped on the comm stream, or inline on the compute stream
     void any_exchange(int n, hipStream_t s) {
-        if (tb_ && !ranks_[0].tb_sends.empty()) exchange_tb(n, s);  // deep x halos
+        if (tb_ && tb_halo(ranks_[0])) exchange_tb(n, s);  // deep halos
         else exchange(n, s);
     }
 
@@ -724,7 +833,7 @@ private:
         } else {
             bool any = false;
             for (auto& R : ranks_)
-                any |= !R.plan.sends.empty() || !R.tb_sends.empty() || fault_.kind == "drop_face";
+                any |= !R.plan.sends.empty() || tb_halo(R) || fault_.kind == "drop_face";
             if (!any) return;
             prof_mark(s_comp_, 2);
             any_exchange(n, s_comp_);
@@ -855,7 +964,7 @@ private:
                     if (R.wrap.src[q] >= 1) copy_plane(R, lp, R.wrap.src[q], R.wrap.dst[q]);
             }
         }
-        if (tb_ && !ranks_[0].tb_sends.empty()) {
+        if (tb_ && tb_halo(ranks_[0])) {
             exchange_tb(n, s_comp_);  // A level = u^n (2 deep + alias), B level = u^{n-1}
         } else {
             for (int l : {n - 1, n}) {

@@ -25,10 +25,9 @@ static void parse_tb(const std::string& name, int& rows, int& waves) {
 
 Layout plan_layout(const Config& c, int world) {
     Layout l;
-    // "auto": temporal blocking (tb2, measured fastest on MI355X, profiles/) whenever the
-    // decomposition allows it (one rank, or x slabs); otherwise the single-step march2.
-    const bool yz_split = c.dims[1] > 1 || c.dims[2] > 1;
-    const bool auto_tb = c.kernel == "auto" && !yz_split;
+    // "auto": temporal blocking (tb2, measured fastest on MI355X, profiles/); across ranks
+    // x slabs unless --dims asks for another decomposition (then 2-deep y/z halos too)
+    const bool auto_tb = c.kernel == "auto";
     l.tb = auto_tb || c.kernel.rfind("tb2", 0) == 0;
     if (l.tb && !auto_tb) parse_tb(c.kernel, l.rows, l.waves);
     l.G = l.tb ? 2 : 1;

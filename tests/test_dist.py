@@ -71,6 +71,17 @@ def test_hip_multiprocess_temporal_blocking(C, single_cpu, P, kernel):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("P,dims", [(8, "2,2,2"), (4, "1,2,2")])
+def test_hip_multiprocess_temporal_blocking_3d(C, single_cpu, P, dims):
+    """Temporal blocking on the reference's 3-D block decomposition (6-face, 3-round deep
+    halos), P processes through the tag-less FIFO staged transport."""
+    r = torchrun(P, ["--backend", "hip", "--transport", "staged", "--shared-device"],
+                 ARGS + ["--dims", dims])
+    assert r["dims"] == [int(x) for x in dims.split(",")] and r["kernel"] == "tb2"
+    assert r["max_abs"] == single_cpu["max_abs"] and r["max_rel"] == single_cpu["max_rel"]
+
+
+@pytest.mark.gpu
 def test_rccl_transport_single_rank(C, single_cpu):
     r = torchrun(1, ["--backend", "hip", "--transport", "rccl"], ARGS)
     assert r["transport"] == "rccl"

@@ -15,8 +15,8 @@ def test_layout_auto_is_temporal_blocking_on_slabs(C):
     assert p8["tb"] and p8["dims"] == [8, 1, 1]
     m = C.memory_plan(ARGS + ["--kernel", "march2"], 8)
     assert not m["tb"] and m["ghost"] == 1 and m["levels"] == 3 and m["dims"] == [0, 0, 0]
-    y = C.memory_plan(ARGS + ["--dims", "2,2,2"], 8)  # y/z split: single-step kernel
-    assert not y["tb"]
+    y = C.memory_plan(ARGS + ["--dims", "2,2,2"], 8)  # temporal blocking with y/z halos
+    assert y["tb"] and y["dims"] == [2, 2, 2]
 
 
 def test_bytes_per_rank_matches_level_formula(C):
