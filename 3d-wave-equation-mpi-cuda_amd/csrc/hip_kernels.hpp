@@ -137,9 +137,10 @@ struct SeamAlias {
 };
 
 // `rows` per lane x `waves` wave64s per workgroup = tile height (tb2_supported()).
-bool tb2_supported(int rows, int waves);
+// `occ` > 0 caps registers so that many waves fit per SIMD (may spill a little).
+bool tb2_supported(int rows, int waves, int occ = 0);
 template <class T>
-void launch_tb2(int rows, int waves, bool first, const T* A, const T* B, T* C, T* D, const GridView& gv,
+void launch_tb2(int rows, int waves, int occ, bool first, const T* A, const T* B, T* C, T* D, const GridView& gv,
                 const Box* boxes, int nbox, const Box& cdom, int ei0, int ei1, const Wrap& wrapC,
                 const Wrap& wrapD, const SeamAlias<T>& alias, const T* tx, const T* ty,
                 const T* tz, const StepCoefs& cC, const StepCoefs& cD, u64* errC, u64* errD,

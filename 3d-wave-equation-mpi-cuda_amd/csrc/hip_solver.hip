@@ -40,9 +40,10 @@ namespace {
 using clk = std::chrono::steady_clock;
 
 // Temporal-blocking variant names: "tb2" (2 rows/lane, 4 waves), "tb2r<R>", "tb2r<R>w<W>".
-std::string tb_name(int rows, int waves) {
-    std::string s = rows == 2 && waves == 4 ? "tb2" : "tb2r" + std::to_string(rows);
-    if (waves != 4) s += "w" + std::to_string(waves);
+std::string tb_name(int rows, int waves, int occ) {
+    std::string s = rows == 2 && waves == 4 && occ == 0 ? "tb2" : "tb2r" + std::to_string(rows);
+    if (waves != 4 || occ) s += "w" + std::to_string(waves);
+    if (occ) s += "o" + std::to_string(occ);
     return s;
 }
 
@@ -111,10 +112,12 @@ public:
         tb_ = lay.tb;
         tb_rows_ = lay.rows;
         tb_waves_ = lay.waves;
+        tb_occ_ = lay.occ;
         G_ = lay.G;
         L_ = lay.L;
         for (int a = 0; a < 3; ++a) cfg_.dims[a] = lay.dims[a];
-        W3D_REQUIRE(!tb_ || tb2_supported(tb_rows_, tb_waves_), "wave3d: unknown kernel variant " + c.kernel);
+        W3D_REQUIRE(!tb_ || tb2_supported(tb_rows_, tb_waves_, tb_occ_),
+                    "wave3d: unknown kernel variant " + c.kernel);
         kind_ = parse_kernel_variant(tb_ ? std::string("auto") : c.kernel);
         naive_.march = false;
         // interior/shell split + comm stream whenever there is a remote halo to hide
@@ -132,7 +135,7 @@ public:
         if (log_on(LogLevel::Info)) {
             for (auto& R : ranks_) {
                 log_msg(LogLevel::Info, R.topo.describe(), " kernel ",
-                        tb_ ? tb_name(tb_rows_, tb_waves_) : kernel_variant_name(kind_), " levels ",
+                        tb_ ? tb_name(tb_rows_, tb_waves_, tb_occ_) : kernel_variant_name(kind_), " levels ",
                         L_, " ghost ", G_, " bytes/level ", R.elems * sizeof(T), " overlap ",
                         overlap_ ? "on" : "off", " transport ",
                         ext_ ? ext_->name() : (world_ > 1 ? "loopback" : "self"));
@@ -155,7 +158,7 @@ public:
         res.Np = world_;
         res.dtype = cfg_.dtype;
         res.backend = "hip";
-        res.kernel = tb_ ? tb_name(tb_rows_, tb_waves_) : kernel_variant_name(kind_);
+        res.kernel = tb_ ? tb_name(tb_rows_, tb_waves_, tb_occ_) : kernel_variant_name(kind_);
         res.courant = prob_.courant;
         res.transport = ext_ ? ext_->name() : (world_ > 1 ? "loopback" : "self");
         for (int a = 0; a < 3; ++a) res.dims[a] = ranks_[0].topo.dims[a];
@@ -556,7 +559,7 @@ private:
             al.prev = R.alias_buf + R.plane_off;
         }
         if (!boxes) boxes = &R.compute, nbox = 1;
-        launch_tb2<T>(tb_rows_, tb_waves_, m == 1, A, B, R.g[lvl(m)], R.g[lvl(m + 1)], R.gv, boxes, nbox,
+        launch_tb2<T>(tb_rows_, tb_waves_, tb_occ_, m == 1, A, B, R.g[lvl(m)], R.g[lvl(m + 1)], R.gv, boxes, nbox,
                       R.cdom, R.error.i0, R.error.i1, R.wrap, R.wrap2, al, R.tx, R.ty, R.tz,
                       coefs(m), coefs(m + 1), R.err + size_t(m) * kSlotsPerLayer,
                       R.err + size_t(m + 1) * kSlotsPerLayer, cfg_.chunk, s);
@@ -984,6 +987,7 @@ private:
     bool tb_ = false;   // temporal blocking (2 layers per sweep)
     int tb_rows_ = 2;
     int tb_waves_ = 4;
+    int tb_occ_ = 0;
     hipGraphExec_t gexec_ = nullptr;  // captured IC + time loop (graph_eligible())
     bool graph_failed_ = false;
     int G_ = 1;         // ghost depth

@@ -66,8 +66,8 @@ struct TbParams {
 // constant, so no value ever moves between registers: a prefetch load lands in the slot it
 // is consumed from two planes later, and the compiler needs no s_waitcnt vmcnt(0) to copy
 // an in-flight register (the rotate-by-copy form serialised every plane on load latency).
-template <class T, bool FIRST, int R, int NW>
-__global__ void __launch_bounds__(NW * 64) k_tb2(const TbParams<T> p) {
+template <class T, bool FIRST, int R, int NW, int WPE = 1>
+__global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WPE, 8))) k_tb2(const TbParams<T> p) {
     constexpr int TJ = NW * R;
     constexpr int AH = TJ + 4, AW = kTK + 4;  // A tile: rows jt-2..jt+TJ+1, cols kb-2..kb+65
     constexpr int CH = TJ + 2, CW = kTK + 2;  // C tile: rows jt-1..jt+TJ,   cols kb-1..kb+64
@@ -339,33 +339,35 @@ __global__ void __launch_bounds__(NW * 64) k_tb2(const TbParams<T> p) {
 
 }  // namespace
 
+// rows x waves (x minimum waves per SIMD: register cap for the compiler, 0 = none)
 template <class T, bool F>
-static void (*tb_kernel(int rows, int waves))(const TbParams<T>) {
-    switch (rows * 100 + waves) {
-        case 204: return k_tb2<T, F, 2, 4>;
-        case 404: return k_tb2<T, F, 4, 4>;
-        case 804: return k_tb2<T, F, 8, 4>;
-        case 208: return k_tb2<T, F, 2, 8>;
-        case 408: return k_tb2<T, F, 4, 8>;
-        case 216: return k_tb2<T, F, 2, 16>;
-        default: throw Error("tb2: unsupported rows x waves " + std::to_string(rows) + "x" +
-                             std::to_string(waves));
+static void (*tb_kernel(int rows, int waves, int occ))(const TbParams<T>) {
+    switch (rows * 1000 + waves * 10 + occ) {
+        case 2040: return k_tb2<T, F, 2, 4>;
+        case 2044: return k_tb2<T, F, 2, 4, 4>;
+        case 2045: return k_tb2<T, F, 2, 4, 5>;
+        case 4040: return k_tb2<T, F, 4, 4>;
+        case 4043: return k_tb2<T, F, 4, 4, 3>;
+        case 8040: return k_tb2<T, F, 8, 4>;
+        case 2080: return k_tb2<T, F, 2, 8>;
+        case 4080: return k_tb2<T, F, 4, 8>;
+        case 2160: return k_tb2<T, F, 2, 16>;
+        default: return nullptr;
     }
 }
 
-bool tb2_supported(int rows, int waves) {
-    const int c = rows * 100 + waves;
-    return c == 204 || c == 404 || c == 804 || c == 208 || c == 408 || c == 216;
+bool tb2_supported(int rows, int waves, int occ) {
+    return tb_kernel<double, false>(rows, waves, occ) != nullptr;
 }
 
 template <class T>
-void launch_tb2(int rows, int waves, bool first, const T* A, const T* B, T* C, T* D, const GridView& gv,
+void launch_tb2(int rows, int waves, int occ, bool first, const T* A, const T* B, T* C, T* D, const GridView& gv,
                 const Box* boxes, int nbox, const Box& cdom, int ei0, int ei1, const Wrap& wrapC,
                 const Wrap& wrapD, const SeamAlias<T>& alias, const T* tx, const T* ty,
                 const T* tz, const StepCoefs& cC, const StepCoefs& cD, u64* errC, u64* errD,
                 int chunk, hipStream_t s) {
     W3D_REQUIRE(gv.G >= 2, "temporal blocking needs ghost depth >= 2");
-    W3D_REQUIRE(tb2_supported(rows, waves), "tb2: unsupported rows x waves");
+    W3D_REQUIRE(tb2_supported(rows, waves, occ), "tb2: unsupported rows x waves x occupancy");
     W3D_REQUIRE(nbox >= 1 && nbox <= kMaxBoxes, "bad box count");
     TbParams<T> p{};
     p.xcd = xcd_swizzle_enabled();
@@ -431,13 +433,13 @@ void launch_tb2(int rows, int waves, bool first, const T* A, const T* B, T* C, T
     }
     p.nbox = nb;
     if (nb == 0) return;
-    auto kern = first ? tb_kernel<T, true>(rows, waves) : tb_kernel<T, false>(rows, waves);
+    auto kern = first ? tb_kernel<T, true>(rows, waves, occ) : tb_kernel<T, false>(rows, waves, occ);
     hipLaunchKernelGGL(kern, dim3(total), dim3(waves * 64), 0, s, p);
     HIP_OK(hipGetLastError());
 }
 
 #define W3D_TB_INST(T)                                                                       \
-    template void launch_tb2<T>(int, int, bool, const T*, const T*, T*, T*, const GridView&,      \
+    template void launch_tb2<T>(int, int, int, bool, const T*, const T*, T*, T*, const GridView&,      \
                                 const Box*, int, const Box&, int, int, const Wrap&,          \
                                 const Wrap&, const SeamAlias<T>&, const T*, const T*,        \
                                 const T*, const StepCoefs&, const StepCoefs&, u64*, u64*,    \

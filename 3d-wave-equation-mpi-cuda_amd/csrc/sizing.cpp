@@ -7,8 +7,8 @@
 
 namespace wave3d {
 
-static void parse_tb(const std::string& name, int& rows, int& waves) {
-    rows = 2, waves = 4;
+static void parse_tb(const std::string& name, int& rows, int& waves, int& occ) {
+    rows = 2, waves = 4, occ = 0;
     std::string s = name.substr(3);
     if (!s.empty() && s[0] == 'r') {
         size_t n = 0;
@@ -20,6 +20,11 @@ static void parse_tb(const std::string& name, int& rows, int& waves) {
         waves = std::stoi(s.substr(1), &n);
         s = s.substr(1 + n);
     }
+    if (!s.empty() && s[0] == 'o') {
+        size_t n = 0;
+        occ = std::stoi(s.substr(1), &n);
+        s = s.substr(1 + n);
+    }
     W3D_REQUIRE(s.empty(), "wave3d: unknown kernel variant " + name);
 }
 
@@ -29,7 +34,7 @@ Layout plan_layout(const Config& c, int world) {
     // x slabs unless --dims asks for another decomposition (then 2-deep y/z halos too)
     const bool auto_tb = c.kernel == "auto";
     l.tb = auto_tb || c.kernel.rfind("tb2", 0) == 0;
-    if (l.tb && !auto_tb) parse_tb(c.kernel, l.rows, l.waves);
+    if (l.tb && !auto_tb) parse_tb(c.kernel, l.rows, l.waves, l.occ);
     l.G = l.tb ? 2 : 1;
     l.L = l.tb ? 4 : 3;
     for (int a = 0; a < 3; ++a) l.dims[a] = c.dims[a];

@@ -13,6 +13,7 @@ namespace wave3d {
 struct Layout {
     bool tb = false;          // temporal blocking (2 layers per sweep)
     int rows = 2, waves = 4;  // TB tile shape
+    int occ = 0;              // TB register cap (min waves per SIMD, 0 = compiler's choice)
     int G = 1;                // ghost depth
     int L = 3;                // time levels
     int dims[3] = {0, 0, 0};  // decomposition override (0 = Dims_create)
