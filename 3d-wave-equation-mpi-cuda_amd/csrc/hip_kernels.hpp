@@ -46,10 +46,10 @@ struct FusedPack {
 
 // Periodic self-wrap fused into the stores (dims[0] == 1): plane `src[q]` is also written
 // to ghost plane `dst[q]` (depth-2 ghosts need 4 pairs). -1 = unused.
-constexpr int kMaxWrap = 4;
+constexpr int kMaxWrap = 6;
 struct Wrap {
-    int src[kMaxWrap] = {-1, -1, -1, -1};
-    int dst[kMaxWrap] = {-1, -1, -1, -1};
+    int src[kMaxWrap] = {-1, -1, -1, -1, -1, -1};
+    int dst[kMaxWrap] = {-1, -1, -1, -1, -1, -1};
 };
 
 // Stencil kernel variant: 2.5-D marching (rows per lane, non-temporal u^{n-2} loads) or
@@ -94,6 +94,35 @@ struct FaceOp {
 template <class T>
 void launch_faces(T* u, const GridView& gv, const FaceOp<T>* ops, int nops, bool to_buf,
                   hipStream_t s);
+
+// Three-layer temporal blocking (hip_tb3.hip): one sweep computes C = u^m (errors only, never
+// stored), D = u^{m+1} and E = u^{m+2} from A = u^{m-1}, B = u^{m-2}. Needs ghost depth >= 3
+// of A and >= 2 of B. Periodic seam: at plane next_i the x+ neighbour of C is the plane nA and
+// the x+ neighbour of D is nC, C evaluated at that partner plane before the sweep
+// (launch_seam_c); mirrored for prev_i. Pointers address logical (0, 0) of a plane.
+template <class T>
+struct SeamPartners {
+    int next_i = -(1 << 30), prev_i = -(1 << 30);
+    const T *nA = nullptr, *nC = nullptr;  // partner A plane, C evaluated there (launch_seam_c)
+    const T *pA = nullptr, *pC = nullptr;
+};
+// C on a seam partner plane: out = C(Ac; x neighbours Am, Ap; u^{m-2} = Bc), 0 outside cdom
+// (logical plane pointers, full storage extent minus the outermost row/column).
+template <class T>
+struct SeamCPlane {
+    T* out = nullptr;
+    const T *Ac = nullptr, *Am = nullptr, *Ap = nullptr, *Bc = nullptr;
+};
+template <class T>
+void launch_seam_c(bool first, const SeamCPlane<T>* ops, int nops, const GridView& gv,
+                   const Box& cdom, const StepCoefs& cC, hipStream_t s);
+bool tb3_supported(int rows, int waves);
+template <class T>
+void launch_tb3(int rows, int waves, bool first, const T* A, const T* B, T* D, T* E,
+                const GridView& gv, const Box* boxes, int nbox, const Box& cdom, int ei0, int ei1,
+                const Wrap& wrapD, const Wrap& wrapE, const SeamPartners<T>& seam, const T* tx,
+                const T* ty, const T* tz, const StepCoefs& cC, const StepCoefs& cD,
+                const StepCoefs& cE, u64* errC, u64* errD, u64* errE, int chunk, hipStream_t s);
 
 // Box halo staging for the temporal-blocking exchange on y/z splits: copy the logical box
 // `b` of a level (origin `grid` = logical (0,0,0), strides of `gv`) to / from a contiguous

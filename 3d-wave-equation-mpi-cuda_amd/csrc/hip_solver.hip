@@ -40,20 +40,24 @@ namespace {
 using clk = std::chrono::steady_clock;
 
 // Temporal-blocking variant names: "tb2" (2 rows/lane, 4 waves), "tb2r<R>", "tb2r<R>w<W>".
-std::string tb_name(int rows, int waves, int occ) {
+std::string tb_name(int rows, int waves, int occ, int depth = 2) {
+    if (depth == 3)
+        return rows == 2 && waves == 8 ? "tb3" : "tb3r" + std::to_string(rows) + "w" + std::to_string(waves);
     std::string s = rows == 2 && waves == 4 && occ == 0 ? "tb2" : "tb2r" + std::to_string(rows);
     if (waves != 4 || occ) s += "w" + std::to_string(waves);
     if (occ) s += "o" + std::to_string(occ);
     return s;
 }
 
+constexpr int kMaxLevels = 5;  // time levels: 3 single-step, 4 tb2, 5 tb3
+
 template <class T>
 struct DevRank {
     Topology topo;
     GridView gv;
     int lead = 0;
-    T* alloc[4] = {nullptr, nullptr, nullptr, nullptr};
-    T* g[4] = {nullptr, nullptr, nullptr, nullptr};  // logical (0,0,0) of each level
+    T* alloc[kMaxLevels] = {};
+    T* g[kMaxLevels] = {};  // logical (0,0,0) of each level
     i64 plane_off = 0;                                 // g - (start of logical plane 0)
     size_t elems = 0;                                  // allocation per level
     T *tx = nullptr, *ty = nullptr, *tz = nullptr;
@@ -65,6 +69,7 @@ struct DevRank {
     int zero_mask = 0;
     Wrap wrap;                   // single-step periodic self-wrap (depth 1)
     Wrap wrap2;                  // depth-2 self-wrap (temporal blocking: IC and D layers)
+    Wrap wrap3;                  // depth-3 self-wrap (three-layer blocking: IC and E layers)
     Box cdom;                    // temporal blocking: where C is a stencil value
     FusedPack<T> pack;           // pointers into sbuf
     // temporal blocking across ranks (x slabs): plane messages, seam alias plane, boxes
@@ -80,12 +85,14 @@ struct DevRank {
     // axes (ghosts included), so edges arrive without diagonal messages
     struct BoxMsg {
         int peer, tag;
-        int level;      // 0 = D level, 1 = C level
+        int level;      // 0 = next A level, 1 = next B level, 2 = seam alias plane (A)
         Box box;
         T* buf;
     };
     std::vector<BoxMsg> tb_bsends[2], tb_brecvs[2];
     T* alias_buf = nullptr;      // one plane: x=N (first x-rank) or x=0 (last x-rank)
+    T* alias_bufB = nullptr;     // the same plane of the B level (three-layer blocking)
+    T* seamc_buf = nullptr;      // two planes: C on the seam partner planes (three-layer)
     Box tb_interior;
     std::vector<Box> tb_shell;
 };
@@ -110,13 +117,15 @@ public:
         // --fill-hbm planner, so a planned N is exactly what gets allocated)
         const Layout lay = plan_layout(c, world_);
         tb_ = lay.tb;
+        tbd_ = lay.depth;
         tb_rows_ = lay.rows;
         tb_waves_ = lay.waves;
         tb_occ_ = lay.occ;
         G_ = lay.G;
         L_ = lay.L;
         for (int a = 0; a < 3; ++a) cfg_.dims[a] = lay.dims[a];
-        W3D_REQUIRE(!tb_ || tb2_supported(tb_rows_, tb_waves_, tb_occ_),
+        W3D_REQUIRE(!tb_ || (tbd_ == 3 ? tb3_supported(tb_rows_, tb_waves_)
+                                        : tb2_supported(tb_rows_, tb_waves_, tb_occ_)),
                     "wave3d: unknown kernel variant " + c.kernel);
         kind_ = parse_kernel_variant(tb_ ? std::string("auto") : c.kernel);
         naive_.march = false;
@@ -135,7 +144,7 @@ public:
         if (log_on(LogLevel::Info)) {
             for (auto& R : ranks_) {
                 log_msg(LogLevel::Info, R.topo.describe(), " kernel ",
-                        tb_ ? tb_name(tb_rows_, tb_waves_, tb_occ_) : kernel_variant_name(kind_), " levels ",
+                        tb_ ? tb_name(tb_rows_, tb_waves_, tb_occ_, tbd_) : kernel_variant_name(kind_), " levels ",
                         L_, " ghost ", G_, " bytes/level ", R.elems * sizeof(T), " overlap ",
                         overlap_ ? "on" : "off", " transport ",
                         ext_ ? ext_->name() : (world_ > 1 ? "loopback" : "self"));
@@ -158,7 +167,7 @@ public:
         res.Np = world_;
         res.dtype = cfg_.dtype;
         res.backend = "hip";
-        res.kernel = tb_ ? tb_name(tb_rows_, tb_waves_, tb_occ_) : kernel_variant_name(kind_);
+        res.kernel = tb_ ? tb_name(tb_rows_, tb_waves_, tb_occ_, tbd_) : kernel_variant_name(kind_);
         res.courant = prob_.courant;
         res.transport = ext_ ? ext_->name() : (world_ > 1 ? "loopback" : "self");
         for (int a = 0; a < 3; ++a) res.dims[a] = ranks_[0].topo.dims[a];
@@ -203,6 +212,7 @@ private:
             R.gv.poff = int(R.plane_off);
             R.lead = int(R.plane_off);
             R.elems = size_t(X + 2 * G_) * size_t(R.gv.si);
+            W3D_REQUIRE(L_ <= kMaxLevels, "too many time levels");
             for (int l = 0; l < L_; ++l) {
                 HIP_CHECK(hipMalloc(&R.alloc[l], R.elems * sizeof(T)));
                 HIP_CHECK(hipMemset(R.alloc[l], 0, R.elems * sizeof(T)));
@@ -247,13 +257,20 @@ private:
                 R.wrap2.src[1] = X - 1, R.wrap2.dst[1] = 0;
                 R.wrap2.src[2] = 2, R.wrap2.dst[2] = X + 1;
                 R.wrap2.src[3] = 3, R.wrap2.dst[3] = X + 2;
+                for (int q = 0; q < 3; ++q) {
+                    R.wrap3.src[q] = X - 3 + q, R.wrap3.dst[q] = -2 + q;
+                    R.wrap3.src[3 + q] = 2 + q, R.wrap3.dst[3 + q] = X + 1 + q;
+                }
+                if (tbd_ == 3) W3D_REQUIRE(X >= 7, "three-layer blocking self-wrap needs >= 7 x planes");
                 if (tb_) W3D_REQUIRE(X >= 5, "temporal blocking self-wrap needs >= 5 x planes");
             }
+            // stencil-valued region of the blocked layers: C/D/E are evaluated on rings up to
+            // G-1 nodes into a neighbour's ghosts; Dirichlet faces (no neighbour) stay 0
             R.cdom = R.compute;
-            if (t.nbr[1][0] >= 0) R.cdom.j0 -= 1;
-            if (t.nbr[1][1] >= 0) R.cdom.j1 += 1;
-            if (t.nbr[2][0] >= 0) R.cdom.k0 -= 1;
-            if (t.nbr[2][1] >= 0) R.cdom.k1 += 1;
+            if (t.nbr[1][0] >= 0) R.cdom.j0 -= G_ - 1;
+            if (t.nbr[1][1] >= 0) R.cdom.j1 += G_ - 1;
+            if (t.nbr[2][0] >= 0) R.cdom.k0 -= G_ - 1;
+            if (t.nbr[2][1] >= 0) R.cdom.k1 += G_ - 1;
             for (size_t m = 0; m < R.plan.sends.size(); ++m) {
                 const auto& f = R.plan.sends[m];
                 if (f.axis == 1) {
@@ -273,6 +290,12 @@ private:
             if (t.nbr[2][1] >= 0) in.k1 = std::min(in.k1, Z - 1);
             R.interior = in;
             build_tb_plan(R);
+            if (tbd_ == 3 && (R.plan.self_x || t.first(0) || t.last(0))) {
+                // C on the seam partner planes (three-layer sweeps); allocated here, never
+                // inside a hipGraph capture
+                HIP_CHECK(hipMalloc(&R.seamc_buf, 2 * R.gv.si * sizeof(T)));
+                HIP_CHECK(hipMemset(R.seamc_buf, 0, 2 * R.gv.si * sizeof(T)));
+            }
             R.shell.clear();
             auto add = [&](Box b) {
                 if (!b.empty()) R.shell.push_back(b);
@@ -293,7 +316,7 @@ private:
 
     void release() {
         for (auto& R : ranks_) {
-            for (int l = 0; l < 4; ++l) (void)hipFree(R.alloc[l]);
+            for (int l = 0; l < kMaxLevels; ++l) (void)hipFree(R.alloc[l]);
             (void)hipFree(R.tx);
             (void)hipFree(R.ty);
             (void)hipFree(R.tz);
@@ -301,6 +324,8 @@ private:
             for (auto* p : R.rbuf) (void)hipFree(p);
             (void)hipFree(R.err);
             (void)hipFree(R.alias_buf);
+            (void)hipFree(R.alias_bufB);
+            (void)hipFree(R.seamc_buf);
             for (int q = 0; q < 2; ++q) {
                 for (auto& m : R.tb_bsends[q]) (void)hipFree(m.buf);
                 for (auto& m : R.tb_brecvs[q]) (void)hipFree(m.buf);
@@ -323,6 +348,9 @@ private:
         return R.g[level] + i64(i) * R.gv.si - R.plane_off;
     }
     int lvl(int n) const { return n % L_; }
+    const Wrap& wrap_depth(const DevRank<T>& R, int d) const {
+        return d >= 3 ? R.wrap3 : (d == 2 ? R.wrap2 : R.wrap);
+    }
 
     int send_plane(const DevRank<T>& R, int side) const {
         return side ? R.topo.x_send_plus() : R.topo.x_send_minus();
@@ -377,33 +405,45 @@ private:
         using M = typename DevRank<T>::PlaneMsg;
         using BM = typename DevRank<T>::BoxMsg;
         // ---- x: whole planes (contiguous, sent in place) ----------------------------------
+        // depth dA of the newest level (next A), dB = dA - 1 of the one before (next B); the
+        // periodic duplicate plane x = N is skipped (mpi_new.cpp:186-187) and shipped to the
+        // other end of the ring as the seam alias plane instead (tags 12/14, 22/24)
+        const int dA = tbd_, dB = tbd_ - 1;
         if (!R.plan.self_x) {
-            W3D_REQUIRE(X >= 4, "temporal blocking needs >= 4 x planes per rank");
+            W3D_REQUIRE(X >= 2 * dA, "temporal blocking needs >= 2 x depth planes per rank");
             const bool first = t.first(0), last = t.last(0);
             const int up = t.nbr[0][1], dn = t.nbr[0][0];
-            R.tb_sends.push_back(M{up, 11, 0, last ? X - 2 : X - 1, 2});
+            const bool aliasB = tbd_ == 3;
+            R.tb_sends.push_back(M{up, 11, 0, last ? X - dA : X - dA + 1, dA});
             if (last) R.tb_sends.push_back(M{up, 12, 0, X, 1});
-            R.tb_sends.push_back(M{up, 13, 1, t.x_send_plus(), 1});
-            R.tb_sends.push_back(M{dn, 21, 0, first ? 2 : 1, 2});
+            R.tb_sends.push_back(M{up, 13, 1, last ? X - dB : X - dB + 1, dB});
+            if (last && aliasB) R.tb_sends.push_back(M{up, 14, 1, X, 1});
+            R.tb_sends.push_back(M{dn, 21, 0, first ? 2 : 1, dA});
             if (first) R.tb_sends.push_back(M{dn, 22, 0, 1, 1});
-            R.tb_sends.push_back(M{dn, 23, 1, t.x_send_minus(), 1});
-            R.tb_recvs.push_back(M{dn, 11, 0, -1, 2});
+            R.tb_sends.push_back(M{dn, 23, 1, first ? 2 : 1, dB});
+            if (first && aliasB) R.tb_sends.push_back(M{dn, 24, 1, 1, 1});
+            R.tb_recvs.push_back(M{dn, 11, 0, 1 - dA, dA});
             if (first) R.tb_recvs.push_back(M{dn, 12, 0, kAliasPlane, 1});
-            R.tb_recvs.push_back(M{dn, 13, 1, 0, 1});
-            R.tb_recvs.push_back(M{up, 21, 0, X + 1, 2});
+            R.tb_recvs.push_back(M{dn, 13, 1, 1 - dB, dB});
+            if (first && aliasB) R.tb_recvs.push_back(M{dn, 14, 1, kAliasPlane, 1});
+            R.tb_recvs.push_back(M{up, 21, 0, X + 1, dA});
             if (last) R.tb_recvs.push_back(M{up, 22, 0, kAliasPlane, 1});
-            R.tb_recvs.push_back(M{up, 23, 1, X + 1, 1});
+            R.tb_recvs.push_back(M{up, 23, 1, X + 1, dB});
+            if (last && aliasB) R.tb_recvs.push_back(M{up, 24, 1, kAliasPlane, 1});
             if (first || last) {
                 HIP_CHECK(hipMalloc(&R.alias_buf, R.gv.si * sizeof(T)));
                 HIP_CHECK(hipMemset(R.alias_buf, 0, R.gv.si * sizeof(T)));
+                if (aliasB) {
+                    HIP_CHECK(hipMalloc(&R.alias_bufB, R.gv.si * sizeof(T)));
+                    HIP_CHECK(hipMemset(R.alias_bufB, 0, R.gv.si * sizeof(T)));
+                }
             }
         }
-        // ---- y (round 0) and z (round 1): D depth 2, C depth 1 ----------------------------
+        // ---- y (round 0) and z (round 1): next A depth dA, next B depth dB ---------------
         const int G = G_;
         for (int ax = 1; ax <= 2; ++ax) {
             if (t.dims[ax] == 1) continue;
             const int n = ax == 1 ? Y : Z;
-            W3D_REQUIRE(n >= 4, "temporal blocking needs >= 4 nodes per rank on split axes");
             auto box = [&](int lo, int hi) {
                 // full extent (ghosts included) on the axes exchanged before this one
                 Box b{1 - G, X + G, 1, Y, 1, Z};
@@ -423,18 +463,35 @@ private:
             auto& V = R.tb_brecvs[ax - 1];
             // sends: down (to dn) then up; receives: from down then from up — the same
             // per-peer order on both sides (tag-less RCCL matching)
-            if (dn >= 0) add(S, dn, base + 1, 0, box(1, 2)), add(S, dn, base + 2, 1, box(1, 1));
-            if (up >= 0) add(S, up, base + 11, 0, box(n - 1, n)), add(S, up, base + 12, 1, box(n, n));
-            if (dn >= 0) add(V, dn, base + 11, 0, box(-1, 0)), add(V, dn, base + 12, 1, box(0, 0));
-            if (up >= 0) add(V, up, base + 1, 0, box(n + 1, n + 2)), add(V, up, base + 2, 1, box(n + 1, n + 1));
+            W3D_REQUIRE(n >= 2 * dA, "temporal blocking needs >= 2 x depth nodes per rank on split axes");
+            if (dn >= 0) add(S, dn, base + 1, 0, box(1, dA)), add(S, dn, base + 2, 1, box(1, dB));
+            if (up >= 0)
+                add(S, up, base + 11, 0, box(n - dA + 1, n)), add(S, up, base + 12, 1, box(n - dB + 1, n));
+            if (dn >= 0) add(V, dn, base + 11, 0, box(1 - dA, 0)), add(V, dn, base + 12, 1, box(1 - dB, 0));
+            if (up >= 0)
+                add(V, up, base + 1, 0, box(n + 1, n + dA)), add(V, up, base + 2, 1, box(n + 1, n + dB));
+            // three-layer sweeps also evaluate C on the seam alias plane (k_seam_c), whose
+            // j/k neighbours at the subdomain edge are ghosts: the alias planes of the y/z
+            // neighbours (same x coordinate, so they hold the same global plane) supply them
+            if (tbd_ == 3 && R.alias_buf) {
+                auto abox = [&](int lo, int hi) {
+                    Box b = box(lo, hi);
+                    b.i0 = b.i1 = 0;
+                    return b;
+                };
+                if (dn >= 0) add(S, dn, base + 3, 2, abox(1, dA));
+                if (up >= 0) add(S, up, base + 13, 2, abox(n - dA + 1, n));
+                if (dn >= 0) add(V, dn, base + 13, 2, abox(1 - dA, 0));
+                if (up >= 0) add(V, up, base + 3, 2, abox(n + 1, n + dA));
+            }
         }
-        // D within 2 nodes of a received ghost depends on it (through C on the ring)
+        // the last layer within dA nodes of a received ghost depends on it (through the rings)
         Box c = R.compute, in = c;
-        if (!R.plan.self_x) in.i0 = std::max(in.i0, 3), in.i1 = std::min(in.i1, X - 2);
-        if (t.nbr[1][0] >= 0) in.j0 = std::max(in.j0, 3);
-        if (t.nbr[1][1] >= 0) in.j1 = std::min(in.j1, Y - 2);
-        if (t.nbr[2][0] >= 0) in.k0 = std::max(in.k0, 3);
-        if (t.nbr[2][1] >= 0) in.k1 = std::min(in.k1, Z - 2);
+        if (!R.plan.self_x) in.i0 = std::max(in.i0, 1 + dA), in.i1 = std::min(in.i1, X - dA);
+        if (t.nbr[1][0] >= 0) in.j0 = std::max(in.j0, 1 + dA);
+        if (t.nbr[1][1] >= 0) in.j1 = std::min(in.j1, Y - dA);
+        if (t.nbr[2][0] >= 0) in.k0 = std::max(in.k0, 1 + dA);
+        if (t.nbr[2][1] >= 0) in.k1 = std::min(in.k1, Z - dA);
         R.tb_interior = in;
         auto add = [&](Box b) {
             if (!b.empty()) R.tb_shell.push_back(b);
@@ -457,7 +514,7 @@ private:
     }
 
     void* tb_ptr(DevRank<T>& R, const typename DevRank<T>::PlaneMsg& m, int mD) {
-        if (m.plane == kAliasPlane) return R.alias_buf;
+        if (m.plane == kAliasPlane) return m.level == 0 ? R.alias_buf : R.alias_bufB;
         return plane(R, lvl(m.level == 0 ? mD : mD - 1 + L_), m.plane);
     }
 
@@ -497,7 +554,9 @@ private:
                 std::vector<BoxCopy<T>> o;
                 for (auto& m : v) {
                     BoxCopy<T> b;
-                    b.grid = R.g[lvl(m.level == 0 ? mD : mD - 1 + L_)];
+                    // level 2 = the seam alias plane (a one-plane buffer at logical i = 0)
+                    b.grid = m.level == 2 ? R.alias_buf + R.plane_off
+                                          : R.g[lvl(m.level == 0 ? mD : mD - 1 + L_)];
                     b.buf = m.buf;
                     b.b = m.box;
                     o.push_back(b);
@@ -565,6 +624,58 @@ private:
                       R.err + size_t(m + 1) * kSlotsPerLayer, cfg_.chunk, s);
     }
 
+    // Three-layer sweep m: C = u^m (registers only), D = u^{m+1}, E = u^{m+2}.
+    SeamPartners<T> seam_partners(DevRank<T>& R, int m, std::vector<SeamCPlane<T>>* ops) {
+        const T* A = R.g[lvl(m + L_ - 1)];
+        const T* B = R.g[lvl(m + L_ - 2)];
+        const i64 si = R.gv.si;
+        const int X = R.topo.X();
+        SeamPartners<T> sp;
+        auto scratch = [&](int q) { return R.seamc_buf + i64(q) * si + R.plane_off; };
+        auto add = [&](int q, const T* Ac, const T* Am, const T* Ap, const T* Bc) {
+            W3D_REQUIRE(R.seamc_buf, "seam C scratch not allocated");
+            SeamCPlane<T> o;
+            o.out = scratch(q), o.Ac = Ac, o.Am = Am, o.Ap = Ap, o.Bc = Bc;
+            if (ops) ops->push_back(o);
+            return scratch(q);
+        };
+        const T* aA = R.alias_buf ? R.alias_buf + R.plane_off : nullptr;
+        const T* aB = R.alias_bufB ? R.alias_bufB + R.plane_off : nullptr;
+        if (R.plan.self_x) {
+            // ghost copy of N-1 (plane 0) sees x=N (plane X); ghost copy of 1 (X+1) sees x=0
+            sp.next_i = 0, sp.nA = A + X * si;
+            sp.nC = add(0, A + X * si, A + (X - 1) * si, A + (X + 1) * si, B + X * si);
+            sp.prev_i = X + 1, sp.pA = A + 1 * si;
+            sp.pC = add(1, A + 1 * si, A + 0 * si, A + 2 * si, B + 1 * si);
+        } else if (R.topo.first(0)) {  // partner x=N lives on the last x-rank (alias planes)
+            sp.next_i = 0, sp.nA = aA;
+            sp.nC = add(0, aA, A + 0 * si, A + 2 * si, aB);
+        } else if (R.topo.last(0)) {   // partner x=0 lives on the first x-rank
+            sp.prev_i = X + 1, sp.pA = aA;
+            sp.pC = add(1, aA, A + (X - 1) * si, A + (X + 1) * si, aB);
+        }
+        return sp;
+    }
+
+    // seam C planes: after the halo of u^{m-1} (they read its ghost / alias planes)
+    void seam_c(DevRank<T>& R, int m, hipStream_t s) {
+        std::vector<SeamCPlane<T>> ops;
+        seam_partners(R, m, &ops);
+        launch_seam_c<T>(m == 1, ops.data(), int(ops.size()), R.gv, R.cdom, coefs(m), s);
+    }
+
+    void sweep3(DevRank<T>& R, int m, hipStream_t s, const Box* boxes = nullptr, int nbox = 0) {
+        const T* A = R.g[lvl(m + L_ - 1)];
+        const T* B = R.g[lvl(m + L_ - 2)];
+        const SeamPartners<T> sp = seam_partners(R, m, nullptr);
+        if (!boxes) boxes = &R.compute, nbox = 1;
+        launch_tb3<T>(tb_rows_, tb_waves_, m == 1, A, B, R.g[lvl(m + 1)], R.g[lvl(m + 2)], R.gv, boxes,
+                      nbox, R.cdom, R.error.i0, R.error.i1, R.wrap2, R.wrap3, sp, R.tx, R.ty, R.tz,
+                      coefs(m), coefs(m + 1), coefs(m + 2), R.err + size_t(m) * kSlotsPerLayer,
+                      R.err + size_t(m + 1) * kSlotsPerLayer, R.err + size_t(m + 2) * kSlotsPerLayer,
+                      cfg_.chunk, s);
+    }
+
     void pack_faces(DevRank<T>& R, int n, hipStream_t s, bool to_buf) {
         FaceOp<T> ops[4];
         int k = 0;
@@ -582,11 +693,13 @@ private:
     }
 
     void inject_after_exchange(DevRank<T>& R, int n, hipStream_t s) {
-        if (fault_.kind == "drop_face" && fault_.hits(R.topo.rank, n))
+        // exchanges follow every sweep: a fault layer inside the sweep hits its exchange
+        const int lo = tbd_ == 3 ? n - 3 : (tb_ ? n - 2 : n - 1);
+        if (fault_.kind == "drop_face" && fault_.hits_range(R.topo.rank, lo, n))
             HIP_CHECK(hipMemsetAsync(plane(R, lvl(n), 0), 0, R.gv.si * sizeof(T), s));
     }
-    void inject_after_compute(DevRank<T>& R, int n, hipStream_t s) {
-        if (fault_.kind == "nan" && fault_.hits(R.topo.rank, n)) {
+    void inject_after_compute(DevRank<T>& R, int n, hipStream_t s, int from = -1) {
+        if (fault_.kind == "nan" && fault_.hits_range(R.topo.rank, (from < 0 ? n : from) - 1, n)) {
             const Box& b = R.compute;
             if (b.empty()) return;
             T* p = R.g[lvl(n)] + i64((b.i0 + b.i1) / 2) * R.gv.si + i64((b.j0 + b.j1) / 2) * R.gv.sj +
@@ -716,7 +829,7 @@ private:
         TraceRange tr("wave3d.ic");
         prof_mark(s_comp_, 0);
         for (auto& R : ranks_) {
-            launch_init<T>(R.g[0], R.gv, R.owned, tb_ ? R.wrap2 : R.wrap, R.tx, R.ty, R.tz, ct_[0],
+            launch_init<T>(R.g[0], R.gv, R.owned, wrap_depth(R, G_), R.tx, R.ty, R.tz, ct_[0],
                            R.err, s_comp_);
             pack_faces(R, 0, s_comp_, true);
         }
@@ -731,8 +844,9 @@ private:
         const int K = prob_.K;
         int done = start - 1;
         for (int n = start; n <= K;) {
-            // temporal blocking: layers n and n+1 in one sweep; a lone last layer single-step
-            const int span = (tb_ && n + 1 <= K) ? 2 : 1;
+            // temporal blocking: 3 (tb3) or 2 layers per sweep; shorter tails use the
+            // two-layer sweep / a single step (the storage has ghosts for the deepest)
+            const int span = (tbd_ == 3 && n + 2 <= K) ? 3 : ((tb_ && n + 1 <= K) ? 2 : 1);
             if (cfg_.print_layers && !cfg_.quiet && ranks_[0].topo.rank == 0)
                 for (int q = n; q < n + span; ++q) std::cout << "calculating layer " << q << "\n";
             prof_mark(s_comp_, 0);
@@ -740,7 +854,26 @@ private:
                 for (auto& R : ranks_)
                     if (q <= L_ || q == start)
                         launch_zero_faces<T>(R.g[lvl(q)], R.gv, R.zero_mask, s_comp_);
-            if (span == 2 && overlap_) {
+            if (span == 3 && overlap_) {
+                for (auto& R : ranks_) {
+                    // periodic self-wrap: the interior spans every x plane, so it reads the seam
+                    // C planes too (at positions that need no remote halo); evaluated again
+                    // after the halo for the shell
+                    if (R.plan.self_x && !R.tb_interior.empty()) seam_c(R, n, s_comp_);
+                    if (!R.tb_interior.empty()) sweep3(R, n, s_comp_, &R.tb_interior, 1);
+                }
+                HIP_CHECK(hipStreamWaitEvent(s_comp_, ev_halo_, 0));
+                for (auto& R : ranks_) {
+                    seam_c(R, n, s_comp_);
+                    if (!R.tb_shell.empty())
+                        sweep3(R, n, s_comp_, R.tb_shell.data(), int(R.tb_shell.size()));
+                }
+            } else if (span == 3) {
+                for (auto& R : ranks_) {
+                    seam_c(R, n, s_comp_);
+                    sweep3(R, n, s_comp_);
+                }
+            } else if (span == 2 && overlap_) {
                 for (auto& R : ranks_)
                     if (!R.tb_interior.empty()) sweep(R, n, s_comp_, &R.tb_interior, 1);
                 HIP_CHECK(hipStreamWaitEvent(s_comp_, ev_halo_, 0));
@@ -761,7 +894,8 @@ private:
                 for (auto& R : ranks_) step_boxes(R, n, &R.compute, 1, kind_, s_comp_);
             }
             for (int q = n; q < n + span; ++q)
-                for (auto& R : ranks_) inject_after_compute(R, q, s_comp_);
+                for (auto& R : ranks_)  // tb3 never stores C = u^n: a fault there goes to u^{n+1}
+                    if (!(span == 3 && q == n)) inject_after_compute(R, q, s_comp_, q == n + 1 && span == 3 ? n : q);
             prof_mark(s_comp_, 1);
             const int last = n + span - 1;
             if (last < K) issue_exchange(last);
@@ -809,6 +943,8 @@ private:
                 if (h) (void)hipGraphDestroy(h);
             }
             if (g) (void)hipGraphDestroy(g);
+            (void)hipStreamSynchronize(s_comp_);
+            (void)hipGetLastError();
             (void)hipGetLastError();
             gexec_ = nullptr;
             graph_failed_ = true;
@@ -960,11 +1096,12 @@ private:
             HIP_CHECK(hipMemcpy(R.alloc[lp], prev.data(), R.elems * sizeof(T), hipMemcpyHostToDevice));
             HIP_CHECK(hipMemcpy(R.alloc[lc], cur.data(), R.elems * sizeof(T), hipMemcpyHostToDevice));
             if (R.plan.self_x) {  // periodic self-wrap ghosts of both levels
-                const Wrap& wc = tb_ ? R.wrap2 : R.wrap;  // u^n is the next A (depth 2 for tb)
+                const Wrap& wc = wrap_depth(R, G_);        // u^n is the next A
+                const Wrap& wp = wrap_depth(R, std::max(1, G_ - 1));
                 for (int q = 0; q < kMaxWrap; ++q)
                     if (wc.src[q] >= 1) copy_plane(R, lc, wc.src[q], wc.dst[q]);
                 for (int q = 0; q < kMaxWrap; ++q)
-                    if (R.wrap.src[q] >= 1) copy_plane(R, lp, R.wrap.src[q], R.wrap.dst[q]);
+                    if (wp.src[q] >= 1) copy_plane(R, lp, wp.src[q], wp.dst[q]);
             }
         }
         if (tb_ && tb_halo(ranks_[0])) {
@@ -988,6 +1125,7 @@ private:
     int tb_rows_ = 2;
     int tb_waves_ = 4;
     int tb_occ_ = 0;
+    int tbd_ = 1;       // layers per sweep (1, 2 or 3)
     hipGraphExec_t gexec_ = nullptr;  // captured IC + time loop (graph_eligible())
     bool graph_failed_ = false;
     int G_ = 1;         // ghost depth

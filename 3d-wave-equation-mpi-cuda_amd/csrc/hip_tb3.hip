@@ -1,0 +1,538 @@
+// Temporal blocking, three leapfrog layers per sweep (TB3) on CDNA4.
+//
+// One sweep reads A = u^{m-1}, B = u^{m-2} and writes only D = u^{m+1} and E = u^{m+2}: the
+// middle layer C = u^m lives in registers and LDS (its errors are still reduced). HBM traffic
+// is 32 B per node per three layers = 10.7 B per layer, against 16 for two-layer blocking and
+// 24 for a single-step kernel.
+//
+// Workgroup = NW wave64s owning a (NW*R rows) x 64 tile of E that marches along i. Layer l is
+// evaluated one plane behind layer l-1, on a (3-l)-node ring around the tile (redundantly with
+// the neighbour tiles; identical operations, so bitwise equal):
+//   iteration i:  stage A(i) (+ 3-node ring) -> barrier
+//                 C(i)   on tile + 2-ring  -> LDS C tile
+//                 D(i-1) on tile + 1-ring  from the C tile written last iteration
+//                 E(i-2) on tile           from the D tile written last iteration
+// Every tile is double-buffered, so one barrier per plane. Register state sits in slots indexed
+// by plane number mod 4 / mod 2 with the i loop unrolled by 4 (no copies of in-flight loads).
+//
+// Periodic seam (the reference keeps both x = 0 and x = N, mpi_new.cpp:170-176): the ghost copy
+// of global N-1 sees x = N as its x+ neighbour and the ghost copy of global 1 sees x = 0 as its
+// x- neighbour. For C that is an A plane in memory (or an alias buffer received from the
+// other end of the x ring); for D it is C at that plane, which the sweep never stores: a
+// small kernel (k_seam_c) evaluates C on the two partner planes into a scratch pair before
+// the sweep, and the seam planes load it like the A partner (separate, rarely taken
+// instantiation of the plane body, so the common path carries no extra registers).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <climits>
+#include <type_traits>
+
+#include "device_common.hpp"
+
+namespace wave3d {
+namespace {
+
+template <class T>
+struct Tb3Params {
+    const T* A;
+    const T* B;
+    T* D;
+    T* E;
+    i64 si;
+    int sj;
+    int poff;
+    int jmin, jmax, kmin, kmax;  // storage bounds (logical)
+    int cj0, cj1, ck0, ck1;      // stencil-valued region of C/D/E (0 outside: Dirichlet)
+    int nbox;
+    BoxLaunch box[kMaxBoxes];
+    int ei0, ei1;
+    int wd_lo[2], wd_hi[2], wd_sh[2];  // self-wrap of D (depth 2) and E (depth 3)
+    int we_lo[2], we_hi[2], we_sh[2];
+    // seam partners (logical plane pointers): at plane an_i the x+ neighbour of C is nA and
+    // the x+ neighbour of D is nC (C at the partner plane); mirrored for ap_i / x-.
+    int an_i, ap_i;
+    const T *nA, *nC, *pA, *pC;
+    const T* tx;
+    const T* ty;
+    const T* tz;
+    T hx2, hy2, hz2, yx2, yy2, yz2;
+    T coefC, coefD, coefE, ctC, ctD, ctE;
+    u64* errC;
+    u64* errD;
+    u64* errE;
+};
+
+template <class T, bool FIRST, int R, int NW>
+__global__ void __launch_bounds__(NW * 64) k_tb3(const Tb3Params<T> p) {
+    constexpr int TJ = NW * R;
+    constexpr int AH = TJ + 6, AW = kTK + 6;  // A tile origin (jt-3, kb-3)
+    constexpr int CH = TJ + 4, CW = kTK + 4;  // C tile origin (jt-2, kb-2)
+    constexpr int DH = TJ + 2, DW = kTK + 2;  // D tile origin (jt-1, kb-1)
+    constexpr int N1 = 2 * kTK + 2 * (TJ + 2);        // 1-ring positions
+    constexpr int N2 = 2 * (kTK + 2) + 2 * (TJ + 4);  // 2-ring positions
+    constexpr int N3 = 2 * (kTK + 4) + 2 * (TJ + 6);  // 3-ring positions (A only)
+    static_assert(N1 <= NW * 64 && N2 <= NW * 64 && N3 <= NW * 64, "rings need more lanes");
+    constexpr unsigned ES = sizeof(T);
+    __shared__ T ldsA[2][AH][AW];
+    __shared__ T ldsC[2][CH][CW];
+    __shared__ T ldsD[2][DH][DW];
+
+    const int bid = blockIdx.x;
+    const int b = find_box(p, bid);
+    const BoxLaunch Bx = p.box[b];
+    int local = bid - Bx.block_begin;
+    const int tk = local % Bx.tiles_k;
+    local /= Bx.tiles_k;
+    const int tj = local % Bx.tiles_j;
+    const int ci = local / Bx.tiles_j;
+    const int kb = Bx.kbase + tk * kTK;
+    const int jt = Bx.j0 + tj * TJ;
+    const int ib = Bx.i0 + ci * Bx.chunk;
+    const int ie = min(Bx.i1, ib + Bx.chunk - 1);
+    const int lane = threadIdx.x & 63;
+    const int q = threadIdx.x;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const i64 si = p.si;
+    const int sj = p.sj;
+    const unsigned pbytes = unsigned(si) * ES;
+
+    auto inb = [&](int j, int k) { return j >= p.jmin && j <= p.jmax && k >= p.kmin && k <= p.kmax; };
+    auto incd = [&](int j, int k) { return j >= p.cj0 && j <= p.cj1 && k >= p.ck0 && k <= p.ck1; };
+    auto boff = [&](int j, int k, bool ok) { return ok ? unsigned(j * sj + k + p.poff) * ES : kOOB; };
+    auto prs = [&](const T* base, int i) { return plane_rsrc(base + (i64(i) * si - p.poff), pbytes); };
+    auto lrs = [&](const T* plane) { return plane_rsrc(plane - p.poff, pbytes); };
+
+    // ---- own nodes ------------------------------------------------------------------------
+    const int k = kb + lane;
+    unsigned oa[R], ob[R], os[R];
+    bool ovalid[R], ocd[R];
+    T oty[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const int j = jt + w * R + r;
+        ocd[r] = incd(j, k);
+        ovalid[r] = k >= Bx.k0 && k <= Bx.k1 && j <= Bx.j1;
+        oa[r] = boff(j, k, inb(j, k));
+        ob[r] = boff(j, k, !FIRST && inb(j, k) && ocd[r]);
+        os[r] = boff(j, k, ovalid[r]);
+        oty[r] = ovalid[r] ? p.ty[j] : T(0);
+    }
+    const T otz = (k >= Bx.k0 && k <= Bx.k1) ? p.tz[k] : T(0);
+
+    // ---- ring positions: d-ring = rows jt-d / jt+TJ-1+d over cols kb-d+1 .. kb+64+d-2, then
+    //      cols kb-d / kb+63+d over rows jt-d .. jt+TJ-1+d -------------------------------------
+    auto ring = [&](int d, int idx, int& rj, int& rk) {
+        const int wd = kTK + 2 * (d - 1), hd = TJ + 2 * d;
+        if (idx < wd) rj = jt - d, rk = kb - (d - 1) + idx;
+        else if (idx < 2 * wd) rj = jt + TJ - 1 + d, rk = kb - (d - 1) + idx - wd;
+        else if (idx < 2 * wd + hd) rj = jt - d + (idx - 2 * wd), rk = kb - d;
+        else rj = jt - d + (idx - 2 * wd - hd), rk = kb + kTK - 1 + d;
+    };
+    int r1j = 0, r1k = 0, r2j = 0, r2k = 0, r3j = 0, r3k = 0;
+    const bool on1 = q < N1, on2 = q < N2, on3 = q < N3;
+    if (on1) ring(1, q, r1j, r1k);
+    if (on2) ring(2, q, r2j, r2k);
+    if (on3) ring(3, q, r3j, r3k);
+    const bool cd1 = on1 && incd(r1j, r1k), cd2 = on2 && incd(r2j, r2k);
+    const unsigned r1a = boff(r1j, r1k, on1 && inb(r1j, r1k));
+    const unsigned r1b = boff(r1j, r1k, !FIRST && on1 && inb(r1j, r1k) && cd1);
+    const unsigned r2a = boff(r2j, r2k, on2 && inb(r2j, r2k));
+    const unsigned r2b = boff(r2j, r2k, !FIRST && on2 && inb(r2j, r2k) && cd2);
+    const unsigned r3a = boff(r3j, r3k, on3 && inb(r3j, r3k));
+    // LDS coordinates (A tile) of the rings
+    const int a1y = r1j - jt + 3, a1x = r1k - kb + 3;
+    const int a2y = r2j - jt + 3, a2x = r2k - kb + 3;
+    const int a3y = r3j - jt + 3, a3x = r3k - kb + 3;
+
+    // slots (iteration i = ib - 2 + q, phase P = q & 3):
+    //   A(x), ring A(x): (x - ib + 3) & 3  -> A(i-1) = P, A(i) = P+1, A(i+1) = P+2, A(i+2) = P+3
+    //   C(x): (x - ib + 2) & 3             -> C(i) = P, C(i-1) = P+3, C(i-2) = P+2
+    //   D(x): (x - ib + 3) & 3             -> D(i-1) = P, D(i-2) = P+3, D(i-3) = P+2
+    //   B(x), 3-ring A(x), LDS buffers: (x - ib + 2) & 1
+    T a[4][R], c[4][R], d[4][R], bb[2][R];
+    T a1[4], c1[4], b1[2], a2[4], b2[2], a3[2];
+    {
+        const auto r0 = prs(p.A, ib - 3), rA1 = prs(p.A, ib - 2), rA2 = prs(p.A, ib - 1);
+        const auto rB = prs(p.B, ib - 2);
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            a[0][r] = bld<T>(r0, oa[r]);
+            a[1][r] = bld<T>(rA1, oa[r]);
+            a[2][r] = bld<T>(rA2, oa[r]);
+            a[3][r] = T(0);
+            bb[0][r] = bld<T>(rB, ob[r]);
+            bb[1][r] = T(0);
+#pragma unroll
+            for (int s = 0; s < 4; ++s) c[s][r] = d[s][r] = T(0);
+        }
+        a1[0] = bld<T>(r0, r1a), a1[1] = bld<T>(rA1, r1a), a1[2] = bld<T>(rA2, r1a), a1[3] = T(0);
+        a2[0] = bld<T>(r0, r2a), a2[1] = bld<T>(rA1, r2a), a2[2] = bld<T>(rA2, r2a), a2[3] = T(0);
+        b1[0] = bld<T>(rB, r1b), b1[1] = T(0);
+        b2[0] = bld<T>(rB, r2b), b2[1] = T(0);
+        a3[0] = bld<T>(rA1, r3a), a3[1] = T(0);
+#pragma unroll
+        for (int s = 0; s < 4; ++s) c1[s] = T(0);
+    }
+
+    T ma1 = T(kErrInit), mr1 = T(kErrInit), ma2 = T(kErrInit), mr2 = T(kErrInit);
+    T ma3 = T(kErrInit), mr3 = T(kErrInit);
+    bool bad1 = false, bad2 = false, bad3 = false;
+
+    auto lapA = [&](int H, int y, int x, T ctr, T xm, T xp) {
+        return laplace7_cr(ctr, xm, xp, ldsA[H][y - 1][x], ldsA[H][y + 1][x], ldsA[H][y][x - 1],
+                           ldsA[H][y][x + 1], p.hx2, p.hy2, p.hz2, p.yx2, p.yy2, p.yz2);
+    };
+    auto cval = [&](T ctr, T bv, T lap) {
+        return FIRST ? taylor_first(ctr, lap, p.coefC) : leapfrog(ctr, bv, lap, p.coefC);
+    };
+
+    auto plane = [&](auto phase, auto alias, const int i) {
+        constexpr int P = decltype(phase)::value;
+        constexpr bool ALIAS = decltype(alias)::value;
+        constexpr int S0 = P & 3, S1 = (P + 1) & 3, S2 = (P + 2) & 3, S3 = (P + 3) & 3;
+        constexpr int H0 = P & 1, H1 = (P + 1) & 1;
+
+        // ---- prefetch A(i+2), 3-ring A(i+1), B(i+1) (0-record descriptors when done) ----
+        {
+            const bool more = i <= ie + 1;
+            const unsigned nb = more ? pbytes : 0u;
+            const int d2 = more ? 2 : 0, d1 = more ? 1 : 0;
+            const auto rA2 = plane_rsrc(p.A + (i64(i + d2) * si - p.poff), nb);
+            const auto rA1 = plane_rsrc(p.A + (i64(i + d1) * si - p.poff), nb);
+            const auto rB1 = plane_rsrc(p.B + (i64(i + d1) * si - p.poff), nb);
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                a[S3][r] = bld<T>(rA2, oa[r]);
+                bb[H1][r] = bld<T>(rB1, ob[r]);
+            }
+            a1[S3] = bld<T>(rA2, r1a);
+            a2[S3] = bld<T>(rA2, r2a);
+            b1[H1] = bld<T>(rB1, r1b);
+            b2[H1] = bld<T>(rB1, r2b);
+            a3[H1] = bld<T>(rA1, r3a);
+        }
+        // ---- stage A(i) --------------------------------------------------------------------
+#pragma unroll
+        for (int r = 0; r < R; ++r) ldsA[H0][3 + w * R + r][3 + lane] = a[S1][r];
+        if (on1) ldsA[H0][a1y][a1x] = a1[S1];
+        if (on2) ldsA[H0][a2y][a2x] = a2[S1];
+        if (on3) ldsA[H0][a3y][a3x] = a3[H0];
+        __syncthreads();
+
+        // ---- seam partners (uniform branch, rare) -------------------------------------------
+        T xnA[R], xpA[R], xnA1 = a1[S2], xpA1 = a1[S0], xnA2 = a2[S2], xpA2 = a2[S0];
+        T cnx[R], cpx[R], cnx1 = c1[S0], cpx1 = c1[S2];
+#pragma unroll
+        for (int r = 0; r < R; ++r) xnA[r] = a[S2][r], xpA[r] = a[S0][r], cnx[r] = c[S0][r], cpx[r] = c[S2][r];
+        if constexpr (ALIAS) {
+            // C(i): A partner as x+ (i == an_i) or x- (i == ap_i) neighbour
+            if (i == p.an_i) {
+                const auto rs = lrs(p.nA);
+#pragma unroll
+                for (int r = 0; r < R; ++r) xnA[r] = bld<T>(rs, oa[r]);
+                xnA1 = bld<T>(rs, r1a);
+                xnA2 = bld<T>(rs, r2a);
+            }
+            if (i == p.ap_i) {
+                const auto rs = lrs(p.pA);
+#pragma unroll
+                for (int r = 0; r < R; ++r) xpA[r] = bld<T>(rs, oa[r]);
+                xpA1 = bld<T>(rs, r1a);
+                xpA2 = bld<T>(rs, r2a);
+            }
+            // D(i-1): C at the partner plane (k_seam_c, before the sweep)
+            if (i - 1 == p.an_i) {
+                const auto rs = lrs(p.nC);
+#pragma unroll
+                for (int r = 0; r < R; ++r) cnx[r] = bld<T>(rs, oa[r]);
+                cnx1 = bld<T>(rs, r1a);
+            }
+            if (i - 1 == p.ap_i) {
+                const auto rs = lrs(p.pC);
+#pragma unroll
+                for (int r = 0; r < R; ++r) cpx[r] = bld<T>(rs, oa[r]);
+                cpx1 = bld<T>(rs, r1a);
+            }
+        }
+
+        // ---- C(i) on tile + 2-ring ----------------------------------------------------------
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const int y = 3 + w * R + r, x = 3 + lane;
+            const T lap = lapA(H0, y, x, a[S1][r], xpA[r], xnA[r]);
+            c[S0][r] = ocd[r] ? cval(a[S1][r], bb[H0][r], lap) : T(0);
+            ldsC[H0][y - 1][x - 1] = c[S0][r];
+        }
+        if (on1) {
+            const T lap = lapA(H0, a1y, a1x, a1[S1], xpA1, xnA1);
+            c1[S0] = cd1 ? cval(a1[S1], b1[H0], lap) : T(0);
+            ldsC[H0][a1y - 1][a1x - 1] = c1[S0];
+        }
+        if (on2) {
+            const T lap = lapA(H0, a2y, a2x, a2[S1], xpA2, xnA2);
+            ldsC[H0][a2y - 1][a2x - 1] = cd2 ? cval(a2[S1], b2[H0], lap) : T(0);
+        }
+        // C errors (own planes)
+        if (i >= ib && i <= ie) {
+            const bool erow = i >= p.ei0 && i <= p.ei1;
+            const T sx = ldconst(p.tx, i);
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                if (!ovalid[r]) continue;
+                bad1 |= nonfinite(c[S0][r]);
+                if (erow) accumulate_error(c[S0][r], analytic(sx, oty[r], otz, p.ctC), ma1, mr1);
+            }
+        }
+        if constexpr (!ALIAS) {
+            // the x neighbours of D(i-1) are C(i) (computed just now) and C(i-2)
+#pragma unroll
+            for (int r = 0; r < R; ++r) cnx[r] = c[S0][r];
+            cnx1 = c1[S0];
+        } else {
+            if (i - 1 != p.an_i) {
+#pragma unroll
+                for (int r = 0; r < R; ++r) cnx[r] = c[S0][r];
+                cnx1 = c1[S0];
+            }
+        }
+
+        // ---- D(i-1) on tile + 1-ring, from the C(i-1) tile --------------------------------
+        const int id = i - 1;
+        if (id >= ib - 1 && id <= ie + 1) {
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                const int y = 2 + w * R + r, x = 2 + lane;  // C tile coordinates
+                const T lap = laplace7_cr(c[S3][r], cpx[r], cnx[r], ldsC[H1][y - 1][x],
+                                          ldsC[H1][y + 1][x], ldsC[H1][y][x - 1], ldsC[H1][y][x + 1],
+                                          p.hx2, p.hy2, p.hz2, p.yx2, p.yy2, p.yz2);
+                d[S0][r] = ocd[r] ? leapfrog(c[S3][r], a[S0][r], lap, p.coefD) : T(0);
+                ldsD[H0][y - 1][x - 1] = d[S0][r];
+            }
+            if (on1) {
+                const int y = a1y - 1, x = a1x - 1;
+                const T lap = laplace7_cr(c1[S3], cpx1, cnx1, ldsC[H1][y - 1][x], ldsC[H1][y + 1][x],
+                                          ldsC[H1][y][x - 1], ldsC[H1][y][x + 1], p.hx2, p.hy2,
+                                          p.hz2, p.yx2, p.yy2, p.yz2);
+                ldsD[H0][y - 1][x - 1] = cd1 ? leapfrog(c1[S3], a1[S0], lap, p.coefD) : T(0);
+            }
+            if (id >= ib && id <= ie) {
+                const auto rd = prs(p.D, id);
+#pragma unroll
+                for (int r = 0; r < R; ++r) bst(d[S0][r], rd, os[r]);
+#pragma unroll
+                for (int g = 0; g < 2; ++g)
+                    if (id >= p.wd_lo[g] && id <= p.wd_hi[g]) {
+                        const auto rw = prs(p.D, id + p.wd_sh[g]);
+#pragma unroll
+                        for (int r = 0; r < R; ++r) bst(d[S0][r], rw, os[r]);
+                    }
+                const bool erow = id >= p.ei0 && id <= p.ei1;
+                const T sx = ldconst(p.tx, id);
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    if (!ovalid[r]) continue;
+                    bad2 |= nonfinite(d[S0][r]);
+                    if (erow) accumulate_error(d[S0][r], analytic(sx, oty[r], otz, p.ctD), ma2, mr2);
+                }
+            }
+        }
+
+        // ---- E(i-2) on the tile, from the D(i-2) tile -----------------------------------------
+        const int ie2 = i - 2;
+        if (ie2 >= ib && ie2 <= ie) {
+            T ev[R];
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                const int y = 1 + w * R + r, x = 1 + lane;  // D tile coordinates
+                const T lap = laplace7_cr(d[S3][r], d[S2][r], d[S0][r], ldsD[H1][y - 1][x],
+                                          ldsD[H1][y + 1][x], ldsD[H1][y][x - 1], ldsD[H1][y][x + 1],
+                                          p.hx2, p.hy2, p.hz2, p.yx2, p.yy2, p.yz2);
+                ev[r] = leapfrog(d[S3][r], c[S2][r], lap, p.coefE);
+            }
+            const auto re = prs(p.E, ie2);
+#pragma unroll
+            for (int r = 0; r < R; ++r) bst(ev[r], re, os[r]);
+#pragma unroll
+            for (int g = 0; g < 2; ++g)
+                if (ie2 >= p.we_lo[g] && ie2 <= p.we_hi[g]) {
+                    const auto rw = prs(p.E, ie2 + p.we_sh[g]);
+#pragma unroll
+                    for (int r = 0; r < R; ++r) bst(ev[r], rw, os[r]);
+                }
+            const bool erow = ie2 >= p.ei0 && ie2 <= p.ei1;
+            const T sx = ldconst(p.tx, ie2);
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                if (!ovalid[r]) continue;
+                bad3 |= nonfinite(ev[r]);
+                if (erow) accumulate_error(ev[r], analytic(sx, oty[r], otz, p.ctE), ma3, mr3);
+            }
+        }
+    };
+
+    auto step = [&](auto phase, const int i) {
+        const bool seam = i == p.an_i || i == p.ap_i || i - 1 == p.an_i || i - 1 == p.ap_i;
+        if (seam) plane(phase, std::true_type{}, i);
+        else plane(phase, std::false_type{}, i);
+    };
+
+    // i = ib-2 .. ie+2 (>= 5 planes), unrolled by 4 so every slot index is a constant
+    for (int i = ib - 2;;) {
+        step(Ph<0>{}, i);
+        if (++i > ie + 2) break;
+        step(Ph<1>{}, i);
+        if (++i > ie + 2) break;
+        step(Ph<2>{}, i);
+        if (++i > ie + 2) break;
+        step(Ph<3>{}, i);
+        if (++i > ie + 2) break;
+    }
+    commit_errors<T, NW>(ma1, mr1, bad1, p.errC);
+    __syncthreads();
+    commit_errors<T, NW>(ma2, mr2, bad2, p.errD);
+    __syncthreads();
+    commit_errors<T, NW>(ma3, mr3, bad3, p.errE);
+}
+
+// C (layer m) on one partner plane of the periodic seam, every (j, k) of the storage except
+// its outermost row/column: out = leapfrog(A_c, B_c, lap) with x neighbours A_m / A_p and
+// j/k neighbours from A_c itself; 0 outside the stencil region. Logical plane pointers.
+template <class T>
+struct SeamCOp {
+    T* out;
+    const T *Ac, *Am, *Ap, *Bc;
+};
+template <class T>
+struct SeamCParams {
+    SeamCOp<T> op[2];
+    int sj, jmin, jmax, kmin, kmax;
+    int cj0, cj1, ck0, ck1;
+    T hx2, hy2, hz2, yx2, yy2, yz2, coef;
+};
+
+template <class T, bool FIRST>
+__global__ void __launch_bounds__(kThreads) k_seam_c(const SeamCParams<T> p) {
+    const SeamCOp<T> o = p.op[blockIdx.y];
+    const int ktiles = (p.kmax - p.kmin - 1 + kTK - 1) / kTK;
+    const int j = p.jmin + 1 + (int(blockIdx.x) / ktiles) * kWaves + int(threadIdx.x >> 6);
+    const int k = p.kmin + 1 + (int(blockIdx.x) % ktiles) * kTK + int(threadIdx.x & 63);
+    if (j > p.jmax - 1 || k > p.kmax - 1) return;
+    const i64 c = i64(j) * p.sj + k;
+    T v = T(0);
+    if (j >= p.cj0 && j <= p.cj1 && k >= p.ck0 && k <= p.ck1) {
+        const T a = o.Ac[c];
+        const T lap = laplace7_cr(a, o.Am[c], o.Ap[c], o.Ac[c - p.sj], o.Ac[c + p.sj], o.Ac[c - 1],
+                                  o.Ac[c + 1], p.hx2, p.hy2, p.hz2, p.yx2, p.yy2, p.yz2);
+        v = FIRST ? taylor_first(a, lap, p.coef) : leapfrog(a, o.Bc[c], lap, p.coef);
+    }
+    o.out[c] = v;
+}
+
+template <class T, bool F>
+static void (*tb3_kernel(int rows, int waves))(const Tb3Params<T>) {
+    switch (rows * 100 + waves) {
+        case 404: return k_tb3<T, F, 4, 4>;
+        case 208: return k_tb3<T, F, 2, 8>;
+        case 204: return k_tb3<T, F, 2, 4>;
+        default: return nullptr;
+    }
+}
+
+}  // namespace
+
+bool tb3_supported(int rows, int waves) { return tb3_kernel<double, false>(rows, waves) != nullptr; }
+
+template <class T>
+void launch_tb3(int rows, int waves, bool first, const T* A, const T* B, T* D, T* E,
+                const GridView& gv, const Box* boxes, int nbox, const Box& cdom, int ei0, int ei1,
+                const Wrap& wrapD, const Wrap& wrapE, const SeamPartners<T>& seam, const T* tx,
+                const T* ty, const T* tz, const StepCoefs& cC, const StepCoefs& cD,
+                const StepCoefs& cE, u64* errC, u64* errD, u64* errE, int chunk, hipStream_t s) {
+    W3D_REQUIRE(gv.G >= 3, "three-layer temporal blocking needs ghost depth >= 3");
+    W3D_REQUIRE(tb3_supported(rows, waves), "tb3: unsupported rows x waves");
+    W3D_REQUIRE(nbox >= 1 && nbox <= kMaxBoxes, "bad box count");
+    Tb3Params<T> p{};
+    p.A = A, p.B = B, p.D = D, p.E = E;
+    p.si = gv.si;
+    p.sj = gv.sj;
+    p.poff = gv.poff;
+    p.jmin = 1 - gv.G, p.jmax = gv.jmax(), p.kmin = 1 - gv.G, p.kmax = gv.kmax();
+    p.cj0 = cdom.j0, p.cj1 = cdom.j1, p.ck0 = cdom.k0, p.ck1 = cdom.k1;
+    p.ei0 = ei0, p.ei1 = ei1;
+    wrap_ranges(wrapD, p.wd_lo, p.wd_hi, p.wd_sh);
+    wrap_ranges(wrapE, p.we_lo, p.we_hi, p.we_sh);
+    p.an_i = seam.nA ? seam.next_i : INT_MIN / 2;
+    p.ap_i = seam.pA ? seam.prev_i : INT_MIN / 2;
+    W3D_REQUIRE((!seam.nA || seam.nC) && (!seam.pA || seam.pC), "tb3: seam partner without its C plane");
+    p.nA = seam.nA, p.nC = seam.nC, p.pA = seam.pA, p.pC = seam.pC;
+    p.tx = tx, p.ty = ty, p.tz = tz;
+    p.hx2 = T(cC.hx2), p.hy2 = T(cC.hy2), p.hz2 = T(cC.hz2);
+    p.yx2 = T(1) / T(cC.hx2), p.yy2 = T(1) / T(cC.hy2), p.yz2 = T(1) / T(cC.hz2);
+    p.coefC = T(cC.coef), p.coefD = T(cD.coef), p.coefE = T(cE.coef);
+    p.ctC = T(cC.ct), p.ctD = T(cD.ct), p.ctE = T(cE.ct);
+    p.errC = errC, p.errD = errD, p.errE = errE;
+    const int TJ = waves * rows;
+    int nb = 0, total = 0;
+    for (int q = 0; q < nbox; ++q) {
+        const Box& bx = boxes[q];
+        if (bx.empty()) continue;
+        W3D_REQUIRE(bx.i0 >= 1 && bx.i1 <= gv.X && bx.j0 >= 1 && bx.j1 <= gv.Y && bx.k0 >= 1 &&
+                        bx.k1 <= gv.Z,
+                    "sweep box outside the owned region");
+        BoxLaunch& L = p.box[nb];
+        L.i0 = bx.i0, L.i1 = bx.i1, L.j0 = bx.j0, L.j1 = bx.j1, L.k0 = bx.k0, L.k1 = bx.k1;
+        const int t0 = (bx.k0 - 1) / kTK, t1 = (bx.k1 - 1) / kTK;
+        L.kbase = 1 + t0 * kTK;
+        L.tiles_k = t1 - t0 + 1;
+        L.tiles_j = cdiv(bx.j1 - bx.j0 + 1, TJ);
+        const int planes = bx.i1 - bx.i0 + 1;
+        const int want = chunk > 0 ? std::min(chunk, planes)
+                                   : auto_chunk(96, planes, L.tiles_k * L.tiles_j);
+        L.chunk = cdiv(planes, cdiv(planes, want));
+        L.block_begin = total;
+        total += L.tiles_k * L.tiles_j * cdiv(planes, L.chunk);
+        ++nb;
+    }
+    p.nbox = nb;
+    if (nb == 0) return;
+    auto kern = first ? tb3_kernel<T, true>(rows, waves) : tb3_kernel<T, false>(rows, waves);
+    hipLaunchKernelGGL(kern, dim3(total), dim3(waves * 64), 0, s, p);
+    HIP_OK(hipGetLastError());
+}
+
+template <class T>
+void launch_seam_c(bool first, const SeamCPlane<T>* ops, int nops, const GridView& gv,
+                   const Box& cdom, const StepCoefs& cC, hipStream_t s) {
+    W3D_REQUIRE(nops >= 0 && nops <= 2, "seam C: at most two planes");
+    if (nops == 0) return;
+    SeamCParams<T> p{};
+    for (int q = 0; q < nops; ++q)
+        p.op[q] = SeamCOp<T>{ops[q].out, ops[q].Ac, ops[q].Am, ops[q].Ap, ops[q].Bc ? ops[q].Bc : ops[q].Ac};
+    p.sj = gv.sj;
+    p.jmin = 1 - gv.G, p.jmax = gv.jmax(), p.kmin = 1 - gv.G, p.kmax = gv.kmax();
+    p.cj0 = cdom.j0, p.cj1 = cdom.j1, p.ck0 = cdom.k0, p.ck1 = cdom.k1;
+    p.hx2 = T(cC.hx2), p.hy2 = T(cC.hy2), p.hz2 = T(cC.hz2);
+    p.yx2 = T(1) / T(cC.hx2), p.yy2 = T(1) / T(cC.hy2), p.yz2 = T(1) / T(cC.hz2);
+    p.coef = T(cC.coef);
+    const int rows = p.jmax - p.jmin - 1, ktiles = cdiv(p.kmax - p.kmin - 1, kTK);
+    const dim3 grid(cdiv(rows, kWaves) * ktiles, nops);
+    void (*kern)(const SeamCParams<T>) = first ? k_seam_c<T, true> : k_seam_c<T, false>;
+    hipLaunchKernelGGL(kern, grid, dim3(kThreads), 0, s, p);
+    HIP_OK(hipGetLastError());
+}
+template void launch_seam_c<double>(bool, const SeamCPlane<double>*, int, const GridView&, const Box&,
+                                    const StepCoefs&, hipStream_t);
+template void launch_seam_c<float>(bool, const SeamCPlane<float>*, int, const GridView&, const Box&,
+                                   const StepCoefs&, hipStream_t);
+
+#define W3D_TB3_INST(T)                                                                       \
+    template void launch_tb3<T>(int, int, bool, const T*, const T*, T*, T*, const GridView&,  \
+                                const Box*, int, const Box&, int, int, const Wrap&,           \
+                                const Wrap&, const SeamPartners<T>&, const T*, const T*,      \
+                                const T*, const StepCoefs&, const StepCoefs&,                 \
+                                const StepCoefs&, u64*, u64*, u64*, int, hipStream_t);
+W3D_TB3_INST(double)
+W3D_TB3_INST(float)
+
+}  // namespace wave3d

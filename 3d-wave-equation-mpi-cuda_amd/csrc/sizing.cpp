@@ -8,7 +8,8 @@
 namespace wave3d {
 
 static void parse_tb(const std::string& name, int& rows, int& waves, int& occ) {
-    rows = 2, waves = 4, occ = 0;
+    if (name.rfind("tb3", 0) != 0) rows = 2, waves = 4;
+    occ = 0;
     std::string s = name.substr(3);
     if (!s.empty() && s[0] == 'r') {
         size_t n = 0;
@@ -33,10 +34,13 @@ Layout plan_layout(const Config& c, int world) {
     // "auto": temporal blocking (tb2, measured fastest on MI355X, profiles/); across ranks
     // x slabs unless --dims asks for another decomposition (then 2-deep y/z halos too)
     const bool auto_tb = c.kernel == "auto";
-    l.tb = auto_tb || c.kernel.rfind("tb2", 0) == 0;
+    const bool tb3 = c.kernel.rfind("tb3", 0) == 0;
+    l.tb = auto_tb || tb3 || c.kernel.rfind("tb2", 0) == 0;
+    l.depth = tb3 ? 3 : (l.tb ? 2 : 1);
+    if (tb3) l.rows = 2, l.waves = 8;  // measured best three-layer tile (profiles/)
     if (l.tb && !auto_tb) parse_tb(c.kernel, l.rows, l.waves, l.occ);
-    l.G = l.tb ? 2 : 1;
-    l.L = l.tb ? 4 : 3;
+    l.G = l.depth;      // ghost depth = layers per sweep
+    l.L = l.depth + 2;  // 3 / 4 / 5 time levels (tb3: C never stored, D and E written)
     for (int a = 0; a < 3; ++a) l.dims[a] = c.dims[a];
     // temporal blocking across ranks: 2-deep x halos, so the decomposition is x slabs
     if (l.tb && world > 1 && !(c.dims[0] || c.dims[1] || c.dims[2])) {

@@ -11,7 +11,8 @@ namespace wave3d {
 
 // Kernel family and storage shape the HIP solver picks for a configuration.
 struct Layout {
-    bool tb = false;          // temporal blocking (2 layers per sweep)
+    bool tb = false;          // temporal blocking
+    int depth = 1;            // layers per sweep: 1 (single step), 2 (tb2) or 3 (tb3)
     int rows = 2, waves = 4;  // TB tile shape
     int occ = 0;              // TB register cap (min waves per SIMD, 0 = compiler's choice)
     int G = 1;                // ghost depth

@@ -43,6 +43,11 @@ struct FaultSpec {
     int layer = -1;
     static FaultSpec parse(const std::string& s);
     bool hits(int r, int n) const { return !kind.empty() && r == rank && n == layer; }
+    // blocked sweeps exchange / store only some layers: a fault on a layer inside (lo, hi]
+    // applies at the next layer that is exchanged / stored
+    bool hits_range(int r, int lo, int hi) const {
+        return !kind.empty() && r == rank && layer > lo && layer <= hi;
+    }
 };
 
 // Early-abort rule for --check-every: a non-finite value was produced on the

@@ -243,3 +243,48 @@ def test_temporal_blocking_3d_fp32_resume(C, tmp_path):
     res = _solve(p, ranks=8, dims=[2, 2, 2], resume=str(tmp_path))
     assert res.extra["resumed_from"] == 12
     assert res.max_abs == full.max_abs and res.max_rel == full.max_rel
+
+
+@pytest.mark.parametrize("kernel", ["tb3", "tb3r2w4", "tb3r4w4"])
+@pytest.mark.parametrize("K", [9, 10, 11])
+def test_tb3_single_rank_bitwise(C, kernel, K):
+    """Three-layer temporal blocking (C never stored, seam partner planes from k_seam_c) with
+    two-layer / single-step tails: bitwise equal to the OpenMP oracle (shifted IC)."""
+    import wave3d
+
+    p = wave3d.WaveProblem(40, Lx=1.3, Ly="pi", Lz=2.0, timesteps=K, ic="shifted")
+    base = _solve(p, backend="cpu", threads=4)
+    r = _solve(p, kernel=kernel)
+    assert r.kernel == kernel
+    assert r.max_abs == base.max_abs and r.max_rel == base.max_rel
+
+
+@pytest.mark.parametrize("ranks,dims,overlap", [(2, None, True), (3, None, False), (4, None, True),
+                                                (8, [2, 2, 2], True), (4, [1, 2, 2], False),
+                                                (2, [1, 1, 2], True)])
+def test_tb3_multi_rank_bitwise(C, ranks, dims, overlap):
+    import wave3d
+
+    for K in (10, 12):
+        p = wave3d.WaveProblem(47, Lx=1.3, Ly="pi", Lz=2.0, timesteps=K, ic="shifted")
+        base = _solve(p, backend="cpu", threads=4)
+        r = _solve(p, ranks=ranks, dims=dims, overlap=overlap, kernel="tb3")
+        assert r.kernel == "tb3"
+        assert r.max_abs == base.max_abs and r.max_rel == base.max_rel
+
+
+def test_tb3_fp32_resume_and_fault(C, tmp_path):
+    import wave3d
+
+    p32 = wave3d.WaveProblem(44, timesteps=13, dtype="fp32", ic="shifted")
+    base = _solve(p32, backend="cpu", threads=4)
+    r = _solve(p32, kernel="tb3")
+    assert r.max_abs == base.max_abs and r.max_rel == base.max_rel
+    p = wave3d.WaveProblem(40, timesteps=14, ic="shifted")
+    full = _solve(p, kernel="tb3", ranks=2)
+    _solve(p, kernel="tb3", ranks=2, checkpoint_every=6, checkpoint_dir=str(tmp_path))
+    res = _solve(p, kernel="tb3", ranks=2, resume=str(tmp_path))
+    assert res.extra["resumed_from"] == 12
+    assert res.max_abs == full.max_abs and res.max_rel == full.max_rel
+    bad = _solve(p, kernel="tb3", ranks=2, fault="nan:1:5", check_every=1)
+    assert bad.aborted
