@@ -17,6 +17,7 @@
 #include <cstring>
 #include <iostream>
 #include <memory>
+#include <thread>
 
 #include "checkpoint.hpp"
 #include "hip_kernels.hpp"
@@ -93,6 +94,7 @@ struct DevRank {
     T* alias_buf = nullptr;      // one plane: x=N (first x-rank) or x=0 (last x-rank)
     T* alias_bufB = nullptr;     // the same plane of the B level (three-layer blocking)
     T* seamc_buf = nullptr;      // two planes: C on the seam partner planes (three-layer)
+    T* pinned = nullptr;         // checkpoint staging (2 levels, pinned host memory)
     Box tb_interior;
     std::vector<Box> tb_shell;
 };
@@ -315,6 +317,10 @@ private:
     }
 
     void release() {
+        if (ckpt_thread_.joinable()) ckpt_thread_.join();
+        if (s_ckpt_) (void)hipStreamDestroy(s_ckpt_);
+        if (ev_ckpt_) (void)hipEventDestroy(ev_ckpt_);
+        s_ckpt_ = nullptr, ev_ckpt_ = nullptr;
         for (auto& R : ranks_) {
             for (int l = 0; l < kMaxLevels; ++l) (void)hipFree(R.alloc[l]);
             (void)hipFree(R.tx);
@@ -326,6 +332,7 @@ private:
             (void)hipFree(R.alias_buf);
             (void)hipFree(R.alias_bufB);
             (void)hipFree(R.seamc_buf);
+            if (R.pinned) (void)hipHostFree(R.pinned);
             for (int q = 0; q < 2; ++q) {
                 for (auto& m : R.tb_bsends[q]) (void)hipFree(m.buf);
                 for (auto& m : R.tb_brecvs[q]) (void)hipFree(m.buf);
@@ -808,6 +815,7 @@ private:
         prof_mark(s_comp_, 5);
         HIP_CHECK(hipEventRecord(ev_end_, s_comp_));
         HIP_CHECK(hipEventSynchronize(ev_end_));
+        finish_checkpoint();  // files complete when solve() returns
         float ms = 0;
         HIP_CHECK(hipEventElapsedTime(&ms, ev_start_, ev_end_));
         tm.total_ms = ms;
@@ -847,6 +855,7 @@ private:
             // temporal blocking: 3 (tb3) or 2 layers per sweep; shorter tails use the
             // two-layer sweep / a single step (the storage has ghosts for the deepest)
             const int span = (tbd_ == 3 && n + 2 <= K) ? 3 : ((tb_ && n + 1 <= K) ? 2 : 1);
+            for (int q = n; q < n + span; ++q) guard_checkpoint_level(lvl(q), s_comp_);
             if (cfg_.print_layers && !cfg_.quiet && ranks_[0].topo.rank == 0)
                 for (int q = n; q < n + span; ++q) std::cout << "calculating layer " << q << "\n";
             prof_mark(s_comp_, 0);
@@ -1048,9 +1057,10 @@ private:
         return a;
     }
 
-    HostLevel host_level(DevRank<T>& R, std::vector<T>& h, int level) {
+    HostLevel host_level(DevRank<T>& R, std::vector<T>& h, int level) { return host_level(R, h.data(), level); }
+    HostLevel host_level(DevRank<T>& R, T* h, int level) {
         HostLevel L;
-        L.origin = h.data() + (R.g[level] - R.alloc[level]);
+        L.origin = h + (R.g[level] - R.alloc[level]);
         L.X = R.topo.X();
         L.Y = R.topo.Y();
         L.Z = R.topo.Z();
@@ -1059,20 +1069,75 @@ private:
         return L;
     }
 
+    // Checkpoint after layer n: the error maxima so far are reduced now (small,
+    // synchronous), the two newest levels are copied device -> pinned host memory on their own
+    // stream while the time loop continues, and a background thread writes the files. The
+    // compute stream only waits for the copy before it overwrites one of those two levels; the
+    // next checkpoint (or the end of the solve) waits for the previous write.
     void save_checkpoints(int n) {
+        TraceRange tr("wave3d.checkpoint");
+        finish_checkpoint();
         std::vector<double> ar = global_errors_upto(n);
         std::vector<double> a(ar.begin(), ar.begin() + prob_.K + 1), r(ar.begin() + prob_.K + 1, ar.end());
-        HIP_CHECK(hipDeviceSynchronize());
+        if (!s_ckpt_) {
+            HIP_CHECK(hipStreamCreateWithFlags(&s_ckpt_, hipStreamNonBlocking));
+            HIP_CHECK(hipEventCreateWithFlags(&ev_ckpt_, hipEventDisableTiming));
+        }
+        std::vector<CheckpointHeader> hs;
+        std::vector<HostLevel> lps, lcs;
         for (auto& R : ranks_) {
             const int lp = lvl(n + L_ - 1), lc = lvl(n);
-            std::vector<T> prev(R.elems), cur(R.elems);
-            HIP_CHECK(hipMemcpy(prev.data(), R.alloc[lp], R.elems * sizeof(T), hipMemcpyDeviceToHost));
-            HIP_CHECK(hipMemcpy(cur.data(), R.alloc[lc], R.elems * sizeof(T), hipMemcpyDeviceToHost));
-            CheckpointHeader h = make_header(cfg_, R.topo, n, sizeof(T));
-            write_checkpoint(cfg_.checkpoint_dir, h, host_level(R, prev, lp), host_level(R, cur, lc),
-                             a, r);
-            log_msg(LogLevel::Info, "rank ", R.topo.rank, ": checkpoint after layer ", n, " -> ",
-                    checkpoint_path(cfg_.checkpoint_dir, R.topo.rank));
+            if (!R.pinned) {
+                void* h = nullptr;
+                HIP_CHECK(hipHostMalloc(&h, 2 * R.elems * sizeof(T), hipHostMallocDefault));
+                R.pinned = static_cast<T*>(h);
+            }
+            HIP_CHECK(hipMemcpyAsync(R.pinned, R.alloc[lp], R.elems * sizeof(T), hipMemcpyDeviceToHost, s_ckpt_));
+            HIP_CHECK(hipMemcpyAsync(R.pinned + R.elems, R.alloc[lc], R.elems * sizeof(T),
+                                     hipMemcpyDeviceToHost, s_ckpt_));
+            hs.push_back(make_header(cfg_, R.topo, n, sizeof(T)));
+            lps.push_back(host_level(R, R.pinned, lp));
+            lcs.push_back(host_level(R, R.pinned + R.elems, lc));
+        }
+        HIP_CHECK(hipEventRecord(ev_ckpt_, s_ckpt_));
+        ckpt_levels_[0] = lvl(n + L_ - 1), ckpt_levels_[1] = lvl(n);
+        ckpt_pending_ = true;
+        int dev = 0;
+        HIP_CHECK(hipGetDevice(&dev));
+        const std::string dir = cfg_.checkpoint_dir;
+        std::vector<int> rk;
+        for (auto& R : ranks_) rk.push_back(R.topo.rank);
+        hipEvent_t ev = ev_ckpt_;
+        ckpt_thread_ = std::thread([=]() {
+            try {
+                (void)hipSetDevice(dev);
+                HIP_CHECK(hipEventSynchronize(ev));
+                for (size_t q = 0; q < hs.size(); ++q) {
+                    write_checkpoint(dir, hs[q], lps[q], lcs[q], a, r);
+                    log_msg(LogLevel::Info, "rank ", rk[q], ": checkpoint after layer ", n, " -> ",
+                            checkpoint_path(dir, rk[q]));
+                }
+            } catch (const std::exception& e) {
+                ckpt_error_ = e.what();
+            }
+        });
+    }
+
+    // the compute stream is about to write `level`: keep the checkpoint copy consistent
+    void guard_checkpoint_level(int level, hipStream_t s) {
+        if (ckpt_pending_ && (level == ckpt_levels_[0] || level == ckpt_levels_[1])) {
+            HIP_CHECK(hipStreamWaitEvent(s, ev_ckpt_, 0));
+            ckpt_pending_ = false;
+        }
+    }
+
+    void finish_checkpoint() {
+        if (ckpt_thread_.joinable()) ckpt_thread_.join();
+        ckpt_pending_ = false;
+        if (!ckpt_error_.empty()) {
+            std::string e = ckpt_error_;
+            ckpt_error_.clear();
+            throw Error("checkpoint write failed: " + e);
         }
     }
 
@@ -1136,6 +1201,12 @@ private:
     std::vector<DevRank<T>> ranks_;
     std::vector<double> ct_;
     std::vector<u64> host_err_;
+    std::thread ckpt_thread_;       // background checkpoint writer
+    std::string ckpt_error_;
+    hipStream_t s_ckpt_ = nullptr;  // device -> pinned host copies of checkpointed levels
+    hipEvent_t ev_ckpt_ = nullptr;
+    bool ckpt_pending_ = false;
+    int ckpt_levels_[2] = {-1, -1};
     std::vector<double> ckpt_abs_, ckpt_rel_;
     hipStream_t s_comp_ = nullptr, s_comm_ = nullptr;
     hipEvent_t ev_start_ = nullptr, ev_end_ = nullptr, ev_layer_ = nullptr, ev_halo_ = nullptr;
