@@ -64,6 +64,10 @@ public:
     // Host doubles, max over ranks (timers).
     virtual void allreduce_max_host(double* data, size_t n) = 0;
     virtual void barrier() = 0;
+    // Wait for `stream` to drain. A transport with asynchronous failure modes (RCCL) polls
+    // its error state and enforces a watchdog timeout here instead of blocking forever;
+    // returns false when the caller should simply synchronise the stream itself.
+    virtual bool wait_stream(void* /*stream*/) { return false; }
 };
 
 }  // namespace wave3d

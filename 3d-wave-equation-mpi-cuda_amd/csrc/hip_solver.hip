@@ -774,7 +774,7 @@ private:
         // in this solve (IC, fused wrap / halo exchange, Dirichlet faces at n <= 3); the
         // buffers are zeroed once at allocation.
         for (auto& R : ranks_) launch_init_err(R.err, K + 1, s_comp_);
-        HIP_CHECK(hipStreamSynchronize(s_comp_));
+        sync(s_comp_);
         if (ext_) ext_->barrier();
 
         res.resumed_from = -1;
@@ -809,7 +809,7 @@ private:
         for (auto& R : ranks_) {
             HIP_CHECK(hipMemcpyAsync(host_err_.data(), R.err, nslot * sizeof(u64),
                                      hipMemcpyDeviceToHost, s_comp_));
-            HIP_CHECK(hipStreamSynchronize(s_comp_));
+            sync(s_comp_);
             for (size_t q = 0; q < nslot; ++q) acc[q] = std::max(acc[q], host_err_[q]);
         }
         prof_mark(s_comp_, 5);
@@ -1013,8 +1013,13 @@ private:
     // Both streams idle: host-side collectives (side stream of the transport) must never run
     // concurrently with an in-flight halo exchange on the same communicator.
     void quiesce() {
-        HIP_CHECK(hipStreamSynchronize(s_comp_));
-        HIP_CHECK(hipStreamSynchronize(s_comm_));
+        sync(s_comp_);
+        sync(s_comm_);
+    }
+
+    // stream drain; with an external transport under its watchdog (RcclTransport)
+    void sync(hipStream_t s) {
+        if (!(ext_ && ext_->wait_stream(s))) HIP_CHECK(hipStreamSynchronize(s));
     }
 
     bool check_layer(int n, RunResult& res) {

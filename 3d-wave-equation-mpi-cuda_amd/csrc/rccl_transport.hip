@@ -10,6 +10,7 @@
 #include <unistd.h>
 
 #include <chrono>
+#include <cstdlib>
 #include <cstring>
 #include <thread>
 #include <vector>
@@ -91,8 +92,7 @@ void RcclTransport::allreduce_max_host(double* data, size_t n) {
                              impl_->side));
     HIP_CHECK_T(hipMemcpyAsync(data, impl_->scratch, n * sizeof(double), hipMemcpyDeviceToHost,
                                impl_->side));
-    HIP_CHECK_T(hipStreamSynchronize(impl_->side));
-    check_async();
+    wait_stream(impl_->side);
 }
 
 void RcclTransport::barrier() {
@@ -104,6 +104,34 @@ void RcclTransport::check_async() const {
     ncclResult_t st = ncclSuccess;
     NCCL_CHECK(ncclCommGetAsyncError(impl_->comm, &st));
     if (st != ncclSuccess) throw Error(std::string("RCCL async error: ") + ncclGetErrorString(st));
+}
+
+bool RcclTransport::wait_stream(void* stream) {
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    static const double limit = [] {
+        const char* e = std::getenv("WAVE3D_WATCHDOG_S");
+        return e ? std::atof(e) : 600.0;
+    }();
+    const auto t0 = std::chrono::steady_clock::now();
+    for (int spin = 0;; ++spin) {
+        const hipError_t q = hipStreamQuery(s);
+        if (q == hipSuccess) break;
+        if (q != hipErrorNotReady) HIP_CHECK_T(q);
+        ncclResult_t st = ncclSuccess;
+        NCCL_CHECK(ncclCommGetAsyncError(impl_->comm, &st));
+        const double el =
+            std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        if (st != ncclSuccess || (limit > 0 && el > limit)) {
+            (void)ncclCommAbort(impl_->comm);
+            impl_->comm = nullptr;
+            throw Error(st != ncclSuccess
+                            ? std::string("RCCL async error: ") + ncclGetErrorString(st)
+                            : "RCCL watchdog: no progress for " + std::to_string(int(el)) +
+                                  " s (WAVE3D_WATCHDOG_S), communicator aborted");
+        }
+        if (spin > 1000) std::this_thread::sleep_for(std::chrono::microseconds(200));
+    }
+    return true;
 }
 
 // ---- TCP rendezvous -------------------------------------------------------------------

@@ -33,6 +33,10 @@ public:
     void barrier() override;
     // Async-error watchdog: throws if the communicator reported an error.
     void check_async() const;
+    // Polls the stream and the communicator's async error; aborts the communicator and throws
+    // after WAVE3D_WATCHDOG_S seconds (default 600) without progress, so a dead peer ends the
+    // run with an error instead of a hang.
+    bool wait_stream(void* stream) override;
 
 private:
     struct Impl;
