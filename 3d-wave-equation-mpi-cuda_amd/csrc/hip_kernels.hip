@@ -329,6 +329,40 @@ __global__ void __launch_bounds__(kThreads) k_naive(const StepParams<T> p) {
 }
 
 // ---------------------------------------------------------------------------------------
+// Flattened kernel for the thin shells of the interior/shell overlap (one plane, row or
+// column wide): one point per thread over each box with k fastest, so a one-column z shell
+// still fills whole waves (a tiled kernel would run 1 of 64 lanes there).
+template <class T, bool FIRST>
+__global__ void __launch_bounds__(kThreads) k_flat(const StepParams<T> p) {
+    const int bid = blockIdx.x;
+    const int b = find_box(p, bid);
+    const BoxLaunch B = p.box[b];
+    const int nk = B.k1 - B.k0 + 1, nj = B.j1 - B.j0 + 1;
+    const i64 total = i64(B.i1 - B.i0 + 1) * nj * nk;
+    const i64 e = i64(bid - B.block_begin) * kThreads + threadIdx.x;
+    T ma = T(kErrInit), mr = T(kErrInit);
+    bool bad = false;
+    if (e < total) {
+        const int k = B.k0 + int(e % nk);
+        const i64 r = e / nk;
+        const int j = B.j0 + int(r % nj);
+        const int i = B.i0 + int(r / nj);
+        const i64 si = p.si;
+        const int rowoff = j * p.sj + k;
+        const i64 o = i64(i) * si + rowoff;
+        const T c = p.u1[o];
+        const T lap = laplace7_cr(c, p.u1[o - si], p.u1[o + si], p.u1[o - p.sj], p.u1[o + p.sj],
+                                  p.u1[o - 1], p.u1[o + 1], p.hx2, p.hy2, p.hz2, p.yx2, p.yy2,
+                                  p.yz2);
+        const T v = FIRST ? taylor_first(c, lap, p.coef) : leapfrog(c, p.u2[o], lap, p.coef);
+        store_point(p, i, j, k, o, rowoff, v);
+        bad |= nonfinite(v);
+        if (i >= p.ei0 && i <= p.ei1) accumulate_error(v, analytic(p.tx[i], p.ty[j], p.tz[k], p.ct), ma, mr);
+    }
+    commit_errors(ma, mr, bad, p.err);
+}
+
+// ---------------------------------------------------------------------------------------
 // Layer 0 (initial condition): one workgroup per 4 x 64 (j,k) tile and `chunk` planes.
 template <class T>
 __global__ void __launch_bounds__(kThreads) k_init(T* u, i64 si, int sj, Box bx, int chunk,
@@ -445,6 +479,10 @@ KernelVariant parse_kernel_variant(const std::string& name) {
         v.march = false;
         return v;
     }
+    if (name == "flat") {
+        v.march = false, v.flat = true;
+        return v;
+    }
     if (name == "auto") {  // best measured single-step variant on MI355X (profiles/)
         v.rows = 2;
         return v;
@@ -462,6 +500,7 @@ KernelVariant parse_kernel_variant(const std::string& name) {
 }
 
 std::string kernel_variant_name(const KernelVariant& v) {
+    if (v.flat) return "flat";
     if (!v.march) return "naive";
     return "march" + std::to_string(v.rows) + (v.nt ? "nt" : "") + (v.fast ? "f" : "") +
            (v.pk ? "p" : "");
@@ -531,9 +570,31 @@ void launch_step(const KernelVariant& kind, bool first, const T* u1, const T* u2
     p.yy2 = T(1) / T(c.hy2);
     p.yz2 = T(1) / T(c.hz2);
     p.err = err;
-    const bool march = kind.march;
+    const bool march = kind.march && !kind.flat;
     const int tj_rows = march ? kWaves * kind.rows : kNaiveTJ;
     int nb = 0, total = 0;
+    if (kind.flat) {
+        for (int q = 0; q < nbox; ++q) {
+            const Box& bx = boxes[q];
+            if (bx.empty()) continue;
+            W3D_REQUIRE(bx.i0 >= 1 && bx.i1 <= gv.X && bx.j0 >= 1 && bx.j1 <= gv.Y && bx.k0 >= 1 &&
+                            bx.k1 <= gv.Z,
+                        "step box outside the owned region");
+            BoxLaunch& L = p.box[nb++];
+            L.i0 = bx.i0, L.i1 = bx.i1, L.j0 = bx.j0, L.j1 = bx.j1, L.k0 = bx.k0, L.k1 = bx.k1;
+            L.kbase = L.tiles_k = L.tiles_j = L.chunk = 1;
+            L.block_begin = total;
+            const i64 pts = i64(bx.i1 - bx.i0 + 1) * (bx.j1 - bx.j0 + 1) * (bx.k1 - bx.k0 + 1);
+            W3D_REQUIRE(pts / kThreads < (1ll << 30), "shell box too large for the flat kernel");
+            total += int((pts + kThreads - 1) / kThreads);
+        }
+        p.nbox = nb;
+        if (nb == 0) return;
+        void (*kern)(const StepParams<T>) = first ? k_flat<T, true> : k_flat<T, false>;
+        hipLaunchKernelGGL(kern, dim3(total), dim3(kThreads), 0, s, p);
+        HIP_OK(hipGetLastError());
+        return;
+    }
     for (int q = 0; q < nbox; ++q) {
         const Box& bx = boxes[q];
         if (bx.empty()) continue;

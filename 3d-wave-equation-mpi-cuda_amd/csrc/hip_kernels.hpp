@@ -60,6 +60,7 @@ struct KernelVariant {
     bool nt = false;
     bool fast = false;  // reciprocal/FMA math: not bitwise-reproducible (benchmark ablation)
     bool pk = false;    // packed fp32: two rows per v_pk_* instruction (fp32 only)
+    bool flat = false;  // one point per thread over the flattened boxes (thin overlap shells)
 };
 KernelVariant parse_kernel_variant(const std::string& name);
 std::string kernel_variant_name(const KernelVariant& v);

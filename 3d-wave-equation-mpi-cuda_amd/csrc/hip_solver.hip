@@ -131,6 +131,7 @@ public:
                     "wave3d: unknown kernel variant " + c.kernel);
         kind_ = parse_kernel_variant(tb_ ? std::string("auto") : c.kernel);
         naive_.march = false;
+        naive_.flat = true;  // thin overlap shells: flattened one-point-per-thread kernel
         // interior/shell split + comm stream whenever there is a remote halo to hide
         overlap_ = c.overlap && (ext_ != nullptr || world_ > 1);
     }
@@ -393,11 +394,12 @@ private:
                        R.err + size_t(n) * kSlotsPerLayer, cfg_.chunk, s);
     }
 
-    // Halo plan of the temporal-blocking path (x slabs; y/z must be Dirichlet):
-    //  up:   D planes (last ? X-2 : X-1)..+1 -> peer ghosts -1..0, [last: D plane X -> peer
-    //        alias], C plane x_send_plus -> peer B-ghost 0
-    //  down: D planes (first ? 2 : 1)..+1  -> peer ghosts X+1..X+2, [first: D plane 1 -> peer
-    //        alias], C plane x_send_minus -> peer B-ghost X+1
+    // Halo plan of the temporal-blocking paths (depth dA = layers per sweep):
+    //  x up:   newest level planes ending at X (last x-rank: at X-1) -> peer ghosts 1-dA..0,
+    //          the level before at depth dA-1, [last: plane X -> peer alias plane(s)]
+    //  x down: mirrored -> peer ghosts X+1..X+dA, [first: plane 1 -> peer alias]
+    //  y, z:   rows / columns staged through buffers, after the x planes, over the full extent
+    //          of the axes exchanged before (edges without diagonal messages)
     // Sends are listed up then down, receives from-down then from-up: per-peer FIFO order
     // matches on both ends also when up == down (dims[0] == 2).
     void build_tb_plan(DevRank<T>& R) {
