@@ -228,7 +228,25 @@ PYBIND11_MODULE(_wave3d_C, m) {
             }
             return result_dict(c, r);
         }, py::arg("args"))
-        .def_property_readonly("init_ms", &Session::init_ms);
+        .def_property_readonly("init_ms", &Session::init_ms)
+        .def("field", [](Session& s, int layer) {
+            std::vector<FieldBlock> bl;
+            {
+                py::gil_scoped_release nogil;
+                bl = s.field(layer);
+            }
+            py::list out;
+            for (auto& b : bl) {
+                py::dict d;
+                d["rank"] = b.rank;
+                d["off"] = std::vector<int>{b.off[0], b.off[1], b.off[2]};
+                d["ext"] = std::vector<int>{b.ext[0], b.ext[1], b.ext[2]};
+                d["data"] = b.data;
+                out.append(d);
+            }
+            return out;
+        }, py::arg("layer"),
+           "Owned blocks (k fastest) of layer K or K-1 after a solve (print_layer analogue).");
 
     m.def("run", &run, py::arg("args"), py::arg("backend") = "hip",
           py::arg("transport") = nullptr, py::arg("write") = true, py::arg("root") = true,

@@ -28,6 +28,7 @@ std::string usage() {
            "  --profile              per-phase timers\n"
            "  --graph on|off|auto    replay the time loop as one hipGraph (auto: when eligible)\n"
            "  --fill-hbm FRAC        GPU program: largest N whose per-GPU footprint fits FRAC of HBM\n"
+           "  --dump PATH            write the final layer u^K as float64 .npy\n"
            "  --fault SPEC           fault injection (drop_face:RANK:LAYER | nan:RANK:LAYER)\n"
            "  --device d  --threads t  --print-layers  --quiet\n";
 }
@@ -157,6 +158,8 @@ Config parse_cli(const std::vector<std::string>& a) {
             c.warmup = parse_int(need(i++), "warmup");
         } else if (o == "--profile") {
             c.profile = true;
+        } else if (o == "--dump") {
+            c.dump = need(i++);
         } else if (o == "--fill-hbm") {
             c.fill_hbm = std::stod(need(i++));
             if (!(c.fill_hbm > 0 && c.fill_hbm <= 0.98)) throw Error("--fill-hbm needs 0 < FRAC <= 0.98");

@@ -54,6 +54,7 @@ struct Config {
     int device = -1;                // explicit device id (default: local rank)
     int threads = 0;                // CPU backend OpenMP threads (0 = Np)
     bool print_layers = false;      // "calculating layer n" lines (reference stdout)
+    std::string dump;               // write the final layer as .npy (print_layer analogue)
 };
 
 // Parse argv; throws wave3d::Error with a usage message on malformed input.

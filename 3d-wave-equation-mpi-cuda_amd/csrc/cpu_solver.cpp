@@ -91,6 +91,24 @@ public:
 
     double init_ms() const { return init_ms_; }
 
+    std::vector<FieldBlock> field(int layer) {
+        const int K = prob_.K;
+        W3D_REQUIRE(layer >= std::max(0, K - 1) && layer <= K, "field: only layers K-1 and K are kept");
+        std::vector<FieldBlock> out;
+        for (auto& R : ranks_) {
+            FieldBlock b;
+            b.rank = R.topo.rank;
+            for (int a = 0; a < 3; ++a) b.off[a] = R.topo.off[a], b.ext[a] = R.topo.ext[a];
+            const auto& u = R.g[layer % 3];
+            b.data.reserve(size_t(b.ext[0]) * b.ext[1] * b.ext[2]);
+            for (int i = 1; i <= b.ext[0]; ++i)
+                for (int j = 1; j <= b.ext[1]; ++j)
+                    for (int k = 1; k <= b.ext[2]; ++k) b.data.push_back(double(u[R.idx(i, j, k)]));
+            out.push_back(std::move(b));
+        }
+        return out;
+    }
+
     RunResult solve_one() {
         RunResult res;
         res.N = prob_.N;
@@ -492,6 +510,7 @@ public:
     CpuSession(const Config& c, Transport* ext) : s_(c, ext) { s_.init(); }
     RunResult solve() override { return s_.solve_one(); }
     double init_ms() const override { return s_.init_ms(); }
+    std::vector<FieldBlock> field(int layer) override { return s_.field(layer); }
 
 private:
     CpuSolver<T> s_;
@@ -514,7 +533,50 @@ RunResult run_session(Session& s, const Config& c) {
         if (last.aborted) break;
     }
     last.solve_ms = times;
+    if (!c.dump.empty() && !last.aborted) dump_field(c.dump, c.N, s.field(c.timesteps), last.nprocs);
     return last;
+}
+
+static void write_npy(const std::string& path, const std::vector<int>& shape, const double* data,
+                      const std::string& comment) {
+    std::string dict = "{'descr': '<f8', 'fortran_order': False, 'shape': (";
+    for (size_t q = 0; q < shape.size(); ++q) dict += std::to_string(shape[q]) + ", ";
+    dict += "), }";
+    if (!comment.empty()) dict += " # " + comment;
+    std::string hdr = dict;
+    while ((10 + hdr.size() + 1) % 64 != 0) hdr += ' ';
+    hdr += '\n';
+    std::FILE* f = std::fopen(path.c_str(), "wb");
+    W3D_REQUIRE(f, "cannot write " + path);
+    const unsigned char magic[8] = {0x93, 'N', 'U', 'M', 'P', 'Y', 1, 0};
+    std::fwrite(magic, 1, 8, f);
+    const unsigned short hl = (unsigned short)hdr.size();
+    std::fwrite(&hl, 2, 1, f);
+    std::fwrite(hdr.data(), 1, hdr.size(), f);
+    size_t n = 1;
+    for (int d : shape) n *= size_t(d);
+    const bool ok = std::fwrite(data, sizeof(double), n, f) == n;
+    std::fclose(f);
+    W3D_REQUIRE(ok, "short write " + path);
+}
+
+void dump_field(const std::string& path, int N, const std::vector<FieldBlock>& blocks, int world) {
+    if (int(blocks.size()) == world) {  // every rank in this process: one global array
+        const size_t n1 = size_t(N) + 1;
+        std::vector<double> g(n1 * n1 * n1, 0.0);
+        for (const auto& b : blocks)
+            for (int i = 0; i < b.ext[0]; ++i)
+                for (int j = 0; j < b.ext[1]; ++j)
+                    std::copy_n(b.data.begin() + (size_t(i) * b.ext[1] + j) * b.ext[2], b.ext[2],
+                                g.begin() + ((b.off[0] + i) * n1 + (b.off[1] + j)) * n1 + b.off[2]);
+        write_npy(path, {int(n1), int(n1), int(n1)}, g.data(), "");
+        return;
+    }
+    for (const auto& b : blocks)
+        write_npy(path + ".r" + std::to_string(b.rank) + ".npy", {b.ext[0], b.ext[1], b.ext[2]},
+                  b.data.data(),
+                  "offset " + std::to_string(b.off[0]) + " " + std::to_string(b.off[1]) + " " +
+                      std::to_string(b.off[2]));
 }
 
 RunResult run_cpu(const Config& c, Transport* external) {

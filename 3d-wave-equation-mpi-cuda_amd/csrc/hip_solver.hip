@@ -186,6 +186,30 @@ public:
         return res;
     }
 
+    // owned block of layer K or K-1 of every local rank (both are always stored)
+    std::vector<FieldBlock> field(int layer) {
+        const int K = prob_.K;
+        W3D_REQUIRE(layer >= std::max(0, K - 1) && layer <= K, "field: only layers K-1 and K are kept");
+        HIP_CHECK(hipDeviceSynchronize());
+        std::vector<FieldBlock> out;
+        for (auto& R : ranks_) {
+            const int l = lvl(layer);
+            std::vector<T> h(R.elems);
+            HIP_CHECK(hipMemcpy(h.data(), R.alloc[l], R.elems * sizeof(T), hipMemcpyDeviceToHost));
+            const HostLevel L = host_level(R, h, l);
+            FieldBlock b;
+            b.rank = R.topo.rank;
+            for (int a = 0; a < 3; ++a) b.off[a] = R.topo.off[a], b.ext[a] = R.topo.ext[a];
+            b.data.reserve(size_t(L.X) * L.Y * L.Z);
+            const T* o = static_cast<const T*>(L.origin);
+            for (int i = 1; i <= L.X; ++i)
+                for (int j = 1; j <= L.Y; ++j)
+                    for (int k = 1; k <= L.Z; ++k) b.data.push_back(double(o[i * L.si + j * L.sj + k]));
+            out.push_back(std::move(b));
+        }
+        return out;
+    }
+
 private:
     // ---- setup ------------------------------------------------------------------------
     void setup() {
@@ -1228,6 +1252,7 @@ public:
     HipSession(const Config& c, Transport* ext) : s_(c, ext) { s_.init(); }
     RunResult solve() override { return s_.solve_one(); }
     double init_ms() const override { return s_.init_ms(); }
+    std::vector<FieldBlock> field(int layer) override { return s_.field(layer); }
 
 private:
     HipSolver<T> s_;

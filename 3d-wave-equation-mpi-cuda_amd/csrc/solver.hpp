@@ -16,6 +16,15 @@
 
 namespace wave3d {
 
+// Owned nodes of one rank's block of a time level, k fastest (the reference's print_layer
+// debug aid, C30: mpi_new.cpp:113-124).
+struct FieldBlock {
+    int rank = 0;
+    int off[3] = {0, 0, 0};  // global index of the block's first node
+    int ext[3] = {0, 0, 0};
+    std::vector<double> data;
+};
+
 // A solver instance: allocation/tables once, then any number of complete solves
 // (IC through layer K + error reduction). Each solve() is one timed benchmark step.
 class Session {
@@ -23,7 +32,13 @@ public:
     virtual ~Session() = default;
     virtual RunResult solve() = 0;
     virtual double init_ms() const = 0;
+    // After a solve: layer K (or K-1) of every rank of this process.
+    virtual std::vector<FieldBlock> field(int layer) = 0;
 };
+
+// Writes the blocks as one (N+1)^3 float64 .npy file (all ranks local) or one file per rank
+// (`path` + ".r<rank>.npy", the block with its offset in the header comment).
+void dump_field(const std::string& path, int N, const std::vector<FieldBlock>& blocks, int world);
 
 std::unique_ptr<Session> make_cpu_session(const Config& c, Transport* external = nullptr);
 std::unique_ptr<Session> make_hip_session(const Config& c, Transport* external = nullptr);

@@ -151,6 +151,26 @@ class WaveSolver:
         o.update(extra)
         return self.problem.args(self.Np, **o)
 
+    def solve_field(self, layer: int | None = None):
+        """One solve, then layer K (default) or K-1 as a NumPy array of the global grid
+        ((N+1)^3, float64) when every rank lives in this process, else this process's blocks
+        (dicts with rank / off / ext / data) — the reference's print_layer debug aid (C30)."""
+        import numpy as np
+
+        C = load()
+        a = self.args()
+        sess = C.Session(a, self.backend, self.transport)
+        res = RunResult.from_dict(sess.solve(a))
+        blocks = sess.field(self.problem.timesteps if layer is None else layer)
+        if len(blocks) != res.nprocs:
+            return res, blocks
+        n1 = self.problem.N + 1
+        g = np.zeros((n1, n1, n1))
+        for b in blocks:
+            (i0, j0, k0), (ni, nj, nk) = b["off"], b["ext"]
+            g[i0:i0 + ni, j0:j0 + nj, k0:k0 + nk] = np.asarray(b["data"]).reshape(ni, nj, nk)
+        return res, g
+
     def run(self, repeat: int = 1, warmup: int = 0, write: bool = False, root: bool = True) -> RunResult:
         C = load()
         a = self.args(repeat=repeat, warmup=warmup or None)

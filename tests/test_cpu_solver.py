@@ -123,3 +123,27 @@ def test_reference_laplacian_exact_on_quadratics():
     u = 0.5 * X * X + 1.5 * Y * Y - Z * Z + 3 * X * Y
     lap = reference.laplace7(u, 1.0, 1.0, 1.0)
     assert torch.allclose(lap, torch.full_like(lap, 1.0 + 3.0 - 2.0), atol=1e-12)
+
+
+def test_field_dump_matches_torch_reference(C, cpu_prog, tmp_path):
+    """Final-layer field access (print_layer analogue): OpenMP ranks, the .npy dump and the
+    plain-PyTorch solve agree bit for bit."""
+    import subprocess
+
+    import numpy as np
+    import torch
+
+    import wave3d
+    from wave3d.ops import reference as R
+
+    N, K = 18, 7
+    p = wave3d.WaveProblem(N, timesteps=K, ic="shifted")
+    res, g = wave3d.WaveSolver(p, "cpu", ranks=3).solve_field()
+    _, _, uK = R.solve(N, K, phase=0.7)
+    ref = uK[1:N + 2].numpy()
+    assert g.shape == (N + 1,) * 3
+    assert np.array_equal(g, ref)
+    path = str(tmp_path / "u.npy")
+    subprocess.run([cpu_prog] + p.args(1) + ["--ranks", "2", "--dump", path, "--format", "none",
+                                              "--quiet"], check=True, cwd=tmp_path)
+    assert np.array_equal(np.load(path), ref)

@@ -288,3 +288,17 @@ def test_tb3_fp32_resume_and_fault(C, tmp_path):
     assert res.max_abs == full.max_abs and res.max_rel == full.max_rel
     bad = _solve(p, kernel="tb3", ranks=2, fault="nan:1:5", check_every=1)
     assert bad.aborted
+
+
+@pytest.mark.parametrize("kernel,ranks,layer", [("auto", 0, None), ("march2", 3, None), ("tb3", 2, None),
+                                                ("tb2", 4, 10), ("flat", 0, None)])
+def test_field_bitwise_vs_cpu(C, kernel, ranks, layer):
+    """The final field itself (not only the error maxima) is bitwise equal to the oracle."""
+    import numpy as np
+
+    import wave3d
+
+    p = wave3d.WaveProblem(33, timesteps=11, ic="shifted")
+    _, ref = wave3d.WaveSolver(p, "cpu", threads=4).solve_field(layer)
+    _, got = wave3d.WaveSolver(p, "hip", kernel=kernel, ranks=ranks).solve_field(layer)
+    assert np.array_equal(got, ref)
