@@ -22,6 +22,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <climits>
 #include <type_traits>
 
@@ -66,7 +67,9 @@ struct TbParams {
 // constant, so no value ever moves between registers: a prefetch load lands in the slot it
 // is consumed from two planes later, and the compiler needs no s_waitcnt vmcnt(0) to copy
 // an in-flight register (the rotate-by-copy form serialised every plane on load latency).
-template <class T, bool FIRST, int R, int NW, int WPE = 1>
+// ABL (measurement ablation, env WAVE3D_TB_ABLATION, not a solver mode): 1 = no error
+// reduction at all, 2 = absolute error only (no relative-error division).
+template <class T, bool FIRST, int R, int NW, int WPE = 1, int ABL = 0>
 __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WPE, 8))) k_tb2(const TbParams<T> p) {
     constexpr int TJ = NW * R;
     constexpr int AH = TJ + 4, AW = kTK + 4;  // A tile: rows jt-2..jt+TJ+1, cols kb-2..kb+65
@@ -274,8 +277,14 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WP
 #pragma unroll
             for (int r = 0; r < R; ++r) {
                 if (!ovalid[r]) continue;
+                if constexpr (ABL == 1) continue;
                 bad1 |= nonfinite(c[S0][r]);
-                if (erow) accumulate_error(c[S0][r], analytic(sx, oty[r], otz, p.ctC), ma1, mr1);
+                if constexpr (ABL == 2) {
+                    if (erow) {
+                        const T e = absval(c[S0][r] - analytic(sx, oty[r], otz, p.ctC));
+                        if (e > ma1) ma1 = e;
+                    }
+                } else if (erow) accumulate_error(c[S0][r], analytic(sx, oty[r], otz, p.ctC), ma1, mr1);
             }
         }
 
@@ -307,8 +316,14 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WP
 #pragma unroll
             for (int r = 0; r < R; ++r) {
                 if (!ovalid[r]) continue;
+                if constexpr (ABL == 1) continue;
                 bad2 |= nonfinite(dv[r]);
-                if (erow) accumulate_error(dv[r], analytic(sx, oty[r], otz, p.ctD), ma2, mr2);
+                if constexpr (ABL == 2) {
+                    if (erow) {
+                        const T e = absval(dv[r] - analytic(sx, oty[r], otz, p.ctD));
+                        if (e > ma2) ma2 = e;
+                    }
+                } else if (erow) accumulate_error(dv[r], analytic(sx, oty[r], otz, p.ctD), ma2, mr2);
             }
         }
     };
@@ -343,7 +358,15 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WP
 template <class T, bool F>
 static void (*tb_kernel(int rows, int waves, int occ))(const TbParams<T>) {
     switch (rows * 1000 + waves * 10 + occ) {
-        case 2040: return k_tb2<T, F, 2, 4>;
+        case 2040: {
+            static const int abl = [] {
+                const char* e = std::getenv("WAVE3D_TB_ABLATION");
+                return e ? std::atoi(e) : 0;
+            }();
+            if (abl == 1) return k_tb2<T, F, 2, 4, 1, 1>;
+            if (abl == 2) return k_tb2<T, F, 2, 4, 1, 2>;
+            return k_tb2<T, F, 2, 4>;
+        }
         case 2044: return k_tb2<T, F, 2, 4, 4>;
         case 2045: return k_tb2<T, F, 2, 4, 5>;
         case 4040: return k_tb2<T, F, 4, 4>;
