@@ -49,6 +49,32 @@ __device__ __forceinline__ T wave_max(T v) {
     return v;
 }
 
+// Running maximum of the relative error |u-f|/|f| without a division per node: the argmax is
+// tracked exactly as the pair (num, den) by comparing num'*den vs num*den' through products
+// split into RN value + exact FMA residual, and the one IEEE division happens at the end.
+// RN is monotone, so value() = RN(max exact quotient) = max of the reference's RN quotients
+// (mpi_new.cpp:341-344): bitwise equal, including its NaN-ignoring `>` and the x/0 = inf case
+// (exact as long as the products are normal numbers, i.e. |errors| and |f| above ~1e-150).
+template <class T>
+struct RelArg {
+    T num = T(kErrInit), den = T(1);
+    __device__ __forceinline__ void add(T ea, T fa) {
+#pragma clang fp contract(off)
+        const T p1 = ea * den, p2 = num * fa;
+        const T e1 = fma_t(ea, den, -p1), e2 = fma_t(num, fa, -p2);
+        if (p1 > p2 || (p1 == p2 && e1 > e2)) num = ea, den = fa;
+    }
+    __device__ __forceinline__ T value() const { return num / den; }
+};
+
+template <class T>
+__device__ __forceinline__ void accumulate_error_dev(T u, T f, T& mabs, RelArg<T>& mrel) {
+#pragma clang fp contract(off)
+    const T ea = absval(u - f);
+    if (ea > mabs) mabs = ea;
+    mrel.add(ea, absval(f));
+}
+
 // Workgroup reduction of the running maxima + one atomic per slot (race-free, no
 // divergent barrier: every thread reaches the __syncthreads, cf. Appendix B5).
 template <class T, int NW = kWaves>

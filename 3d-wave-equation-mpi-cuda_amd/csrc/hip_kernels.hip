@@ -179,7 +179,8 @@ __global__ void __launch_bounds__(kThreads) k_march(const StepParams<T> p) {
     const V yx2 = vsplat<L, V>(p.yx2), yy2 = vsplat<L, V>(p.yy2), yz2 = vsplat<L, V>(p.yz2);
     const V coef = vsplat<L, V>(p.coef), ctv = vsplat<L, V>(p.ct);
 
-    T ma = T(kErrInit), mr = T(kErrInit);
+    T ma = T(kErrInit);
+    RelArg<T> mr;
     bool bad = false;
 
     auto plane = [&](auto phase, const int i) {
@@ -269,8 +270,8 @@ __global__ void __launch_bounds__(kThreads) k_march(const StepParams<T> p) {
                 if (j == p.yj1) p.ybuf1[i64(i - 1) * p.yrow + k] = x;
                 bad |= nonfinite(x);
                 if (erow) {
-                    if constexpr (FAST) accumulate_error_fast(x, vget<L>(f, e), ma, mr);
-                    else accumulate_error(x, vget<L>(f, e), ma, mr);
+                    if constexpr (FAST) accumulate_error_dev(x, vget<L>(f, e), ma, mr);
+                    else accumulate_error_dev(x, vget<L>(f, e), ma, mr);
                 }
             }
         }
@@ -286,7 +287,7 @@ __global__ void __launch_bounds__(kThreads) k_march(const StepParams<T> p) {
         plane(Ph<3>{}, i);
         if (++i > ie) break;
     }
-    commit_errors(ma, mr, bad, p.err);
+    commit_errors(ma, mr.value(), bad, p.err);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -306,7 +307,8 @@ __global__ void __launch_bounds__(kThreads) k_naive(const StepParams<T> p) {
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int k = B.kbase + tk * kTK + lane;
     const int j = B.j0 + tj * kNaiveTJ + w;
-    T ma = T(kErrInit), mr = T(kErrInit);
+    T ma = T(kErrInit);
+    RelArg<T> mr;
     bool bad = false;
     if (k >= B.k0 && k <= B.k1 && j <= B.j1) {
         const i64 si = p.si;
@@ -322,10 +324,10 @@ __global__ void __launch_bounds__(kThreads) k_naive(const StepParams<T> p) {
             store_point(p, i, j, k, o, rowoff, v);
             bad |= nonfinite(v);
             if (i >= p.ei0 && i <= p.ei1)
-                accumulate_error(v, analytic(p.tx[i], tyj, tzk, p.ct), ma, mr);
+                accumulate_error_dev(v, analytic(p.tx[i], tyj, tzk, p.ct), ma, mr);
         }
     }
-    commit_errors(ma, mr, bad, p.err);
+    commit_errors(ma, mr.value(), bad, p.err);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -340,7 +342,8 @@ __global__ void __launch_bounds__(kThreads) k_flat(const StepParams<T> p) {
     const int nk = B.k1 - B.k0 + 1, nj = B.j1 - B.j0 + 1;
     const i64 total = i64(B.i1 - B.i0 + 1) * nj * nk;
     const i64 e = i64(bid - B.block_begin) * kThreads + threadIdx.x;
-    T ma = T(kErrInit), mr = T(kErrInit);
+    T ma = T(kErrInit);
+    RelArg<T> mr;
     bool bad = false;
     if (e < total) {
         const int k = B.k0 + int(e % nk);
@@ -357,9 +360,9 @@ __global__ void __launch_bounds__(kThreads) k_flat(const StepParams<T> p) {
         const T v = FIRST ? taylor_first(c, lap, p.coef) : leapfrog(c, p.u2[o], lap, p.coef);
         store_point(p, i, j, k, o, rowoff, v);
         bad |= nonfinite(v);
-        if (i >= p.ei0 && i <= p.ei1) accumulate_error(v, analytic(p.tx[i], p.ty[j], p.tz[k], p.ct), ma, mr);
+        if (i >= p.ei0 && i <= p.ei1) accumulate_error_dev(v, analytic(p.tx[i], p.ty[j], p.tz[k], p.ct), ma, mr);
     }
-    commit_errors(ma, mr, bad, p.err);
+    commit_errors(ma, mr.value(), bad, p.err);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -372,7 +375,8 @@ __global__ void __launch_bounds__(kThreads) k_init(T* u, i64 si, int sj, Box bx,
     const int j = bx.j0 + blockIdx.y * kWaves + (threadIdx.x >> 6);
     const int ib = bx.i0 + blockIdx.z * chunk;
     const int ie = min(bx.i1, ib + chunk - 1);
-    T ma = T(kErrInit), mr = T(kErrInit);
+    T ma = T(kErrInit);
+    RelArg<T> mr;
     bool bad = false;
     if (k <= bx.k1 && j <= bx.j1) {
         const int rowoff = j * sj + k;
@@ -384,10 +388,10 @@ __global__ void __launch_bounds__(kThreads) k_init(T* u, i64 si, int sj, Box bx,
             for (int q = 0; q < kMaxWrap; ++q)
                 if (i == wrap.src[q]) u[i64(wrap.dst[q]) * si + rowoff] = f;
             bad |= nonfinite(f);
-            accumulate_error(f, analytic(tx[i], tyj, tzk, ct), ma, mr);
+            accumulate_error_dev(f, analytic(tx[i], tyj, tzk, ct), ma, mr);
         }
     }
-    commit_errors(ma, mr, bad, err);
+    commit_errors(ma, mr.value(), bad, err);
 }
 
 template <class T>

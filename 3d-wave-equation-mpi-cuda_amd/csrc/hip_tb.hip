@@ -178,7 +178,8 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WP
         ua[1] = T(0);
     }
 
-    T ma1 = T(kErrInit), mr1 = T(kErrInit), ma2 = T(kErrInit), mr2 = T(kErrInit);
+    T ma1 = T(kErrInit), ma2 = T(kErrInit);
+    RelArg<T> mr1, mr2;
     bool bad1 = false, bad2 = false;
 
     // prefetch A(i+2) (own, ring), A(i+1) (outer ring), B(i+1); on the last plane the
@@ -284,7 +285,7 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WP
                         const T e = absval(c[S0][r] - analytic(sx, oty[r], otz, p.ctC));
                         if (e > ma1) ma1 = e;
                     }
-                } else if (erow) accumulate_error(c[S0][r], analytic(sx, oty[r], otz, p.ctC), ma1, mr1);
+                } else if (erow) accumulate_error_dev(c[S0][r], analytic(sx, oty[r], otz, p.ctC), ma1, mr1);
             }
         }
 
@@ -323,7 +324,7 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WP
                         const T e = absval(dv[r] - analytic(sx, oty[r], otz, p.ctD));
                         if (e > ma2) ma2 = e;
                     }
-                } else if (erow) accumulate_error(dv[r], analytic(sx, oty[r], otz, p.ctD), ma2, mr2);
+                } else if (erow) accumulate_error_dev(dv[r], analytic(sx, oty[r], otz, p.ctD), ma2, mr2);
             }
         }
     };
@@ -347,9 +348,9 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WP
         plane(Ph<3>{}, i);
         if (++i > ie + 1) break;
     }
-    commit_errors<T, NW>(ma1, mr1, bad1, p.errC);
+    commit_errors<T, NW>(ma1, mr1.value(), bad1, p.errC);
     __syncthreads();
-    commit_errors<T, NW>(ma2, mr2, bad2, p.errD);
+    commit_errors<T, NW>(ma2, mr2.value(), bad2, p.errD);
 }
 
 }  // namespace

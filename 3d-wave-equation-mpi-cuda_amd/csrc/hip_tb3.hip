@@ -175,8 +175,10 @@ __global__ void __launch_bounds__(NW * 64) k_tb3(const Tb3Params<T> p) {
         for (int s = 0; s < 4; ++s) c1[s] = T(0);
     }
 
-    T ma1 = T(kErrInit), mr1 = T(kErrInit), ma2 = T(kErrInit), mr2 = T(kErrInit);
-    T ma3 = T(kErrInit), mr3 = T(kErrInit);
+    T ma1 = T(kErrInit), ma2 = T(kErrInit);
+    RelArg<T> mr1, mr2;
+    T ma3 = T(kErrInit);
+    RelArg<T> mr3;
     bool bad1 = false, bad2 = false, bad3 = false;
 
     auto lapA = [&](int H, int y, int x, T ctr, T xm, T xp) {
@@ -281,7 +283,7 @@ __global__ void __launch_bounds__(NW * 64) k_tb3(const Tb3Params<T> p) {
             for (int r = 0; r < R; ++r) {
                 if (!ovalid[r]) continue;
                 bad1 |= nonfinite(c[S0][r]);
-                if (erow) accumulate_error(c[S0][r], analytic(sx, oty[r], otz, p.ctC), ma1, mr1);
+                if (erow) accumulate_error_dev(c[S0][r], analytic(sx, oty[r], otz, p.ctC), ma1, mr1);
             }
         }
         if constexpr (!ALIAS) {
@@ -333,7 +335,7 @@ __global__ void __launch_bounds__(NW * 64) k_tb3(const Tb3Params<T> p) {
                 for (int r = 0; r < R; ++r) {
                     if (!ovalid[r]) continue;
                     bad2 |= nonfinite(d[S0][r]);
-                    if (erow) accumulate_error(d[S0][r], analytic(sx, oty[r], otz, p.ctD), ma2, mr2);
+                    if (erow) accumulate_error_dev(d[S0][r], analytic(sx, oty[r], otz, p.ctD), ma2, mr2);
                 }
             }
         }
@@ -366,7 +368,7 @@ __global__ void __launch_bounds__(NW * 64) k_tb3(const Tb3Params<T> p) {
             for (int r = 0; r < R; ++r) {
                 if (!ovalid[r]) continue;
                 bad3 |= nonfinite(ev[r]);
-                if (erow) accumulate_error(ev[r], analytic(sx, oty[r], otz, p.ctE), ma3, mr3);
+                if (erow) accumulate_error_dev(ev[r], analytic(sx, oty[r], otz, p.ctE), ma3, mr3);
             }
         }
     };
@@ -388,11 +390,11 @@ __global__ void __launch_bounds__(NW * 64) k_tb3(const Tb3Params<T> p) {
         step(Ph<3>{}, i);
         if (++i > ie + 2) break;
     }
-    commit_errors<T, NW>(ma1, mr1, bad1, p.errC);
+    commit_errors<T, NW>(ma1, mr1.value(), bad1, p.errC);
     __syncthreads();
-    commit_errors<T, NW>(ma2, mr2, bad2, p.errD);
+    commit_errors<T, NW>(ma2, mr2.value(), bad2, p.errD);
     __syncthreads();
-    commit_errors<T, NW>(ma3, mr3, bad3, p.errE);
+    commit_errors<T, NW>(ma3, mr3.value(), bad3, p.errE);
 }
 
 // C (layer m) on one partner plane of the periodic seam, every (j, k) of the storage except
