@@ -16,7 +16,8 @@ std::string usage() {
            "  --ranks P              simulate P ranks in-process (loopback transport)\n"
            "  --transport auto|rccl|loopback\n"
            "  --no-overlap           no interior/shell split\n"
-           "  --kernel auto|march|naive|tb2   stencil kernel variant\n"
+           "  --kernel K             auto (= tb2) | tb2[r<R>][w<W>] | tb3[r<R>w<W>] | march[2|4|8][nt|p|f]\n"
+           "                         | naive | flat   (temporal blocking / single-step variants)\n"
            "  --chunk C              i-planes per marching work item\n"
            "  --format new|omp|cuda|none      output file flavour (default new)\n"
            "  --out-dir D  --out-name F\n"
@@ -82,7 +83,7 @@ Config parse_cli(const std::vector<std::string>& a) {
     } catch (const std::exception& e) {
         throw Error(std::string("wave3d: bad positional argument (") + e.what() + ")\n" + usage());
     }
-    W3D_REQUIRE(c.N >= 2, "N must be >= 2");
+    W3D_REQUIRE(c.N >= 2 || c.N == 0, "N must be >= 2 (0 only with --fill-hbm)");
     W3D_REQUIRE(c.Np >= 1, "Np must be >= 1");
     W3D_REQUIRE(c.timesteps >= 1, "timesteps must be >= 1");
     W3D_REQUIRE(c.T > 0, "T must be positive");
@@ -189,6 +190,7 @@ Config parse_cli(const std::vector<std::string>& a) {
     if (c.fault.empty()) {
         if (const char* e = std::getenv("WAVE_FI")) c.fault = e;
     }
+    W3D_REQUIRE(c.N >= 2 || c.fill_hbm > 0, "N must be >= 2 (0 only with --fill-hbm)");
     return c;
 }
 
