@@ -138,7 +138,7 @@ def main() -> int:
         "warmup": a.warmup,
         "ms_per_step": round(elapsed / a.steps * 1e3, 4),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if a.N else "weak",  # --N fixes the global grid
         "vs_baseline": round(value / base, 3),
         "dtype": a.dtype,
         "data": "synthetic (analytic initial condition u=sin(2pi x/Lx)sin(pi y/Ly)sin(pi z/Lz))",
