@@ -21,15 +21,16 @@ GOLDEN_LINF = {
 
 CONFIGS = {
     # N=128^3 fp64 single-process OpenMP (openmp_sol path, plumbing)
-    "cpu128": dict(problem=WaveProblem(128, timesteps=20), backend="cpu", Np=8),
+    "cpu128": dict(problem=WaveProblem(128, timesteps=20), backend="cpu", Np=8, dims=None),
     # N=512^3 fp64 on one MI355X
-    "gpu512": dict(problem=WaveProblem(512, timesteps=100), backend="hip", Np=1),
+    "gpu512": dict(problem=WaveProblem(512, timesteps=100), backend="hip", Np=1, dims=None),
     # N=512^3 fp64 on 2 MI355X, slab decomposition (2x1x1)
-    "gpu512x2": dict(problem=WaveProblem(512, timesteps=100), backend="hip", Np=2),
-    # N=1024^3 fp64 on 8 MI355X, 2x2x2 blocks
-    "gpu1024x8": dict(problem=WaveProblem(1024, timesteps=100), backend="hip", Np=8),
+    "gpu512x2": dict(problem=WaveProblem(512, timesteps=100), backend="hip", Np=2, dims=[2, 1, 1]),
+    # N=1024^3 fp64 on 8 MI355X, 2x2x2 blocks (6-face deep halos, interior/shell overlap)
+    "gpu1024x8": dict(problem=WaveProblem(1024, timesteps=100), backend="hip", Np=8, dims=[2, 2, 2]),
     # N=2048^3 fp32 on 8 MI355X
-    "gpu2048x8_fp32": dict(problem=WaveProblem(2048, timesteps=200, dtype="fp32"), backend="hip", Np=8),
+    "gpu2048x8_fp32": dict(problem=WaveProblem(2048, timesteps=200, dtype="fp32"), backend="hip", Np=8,
+                           dims=None),
 }
 
 
