@@ -167,7 +167,12 @@ def main() -> int:
         out["profile_ms"] = {k: res[k] for k in ("loop_ms", "exchange_ms", "error_ms", "total_ms")}
     if rank == 0:
         print(json.dumps(out), flush=True)
+    # explicit teardown while HIP and the process group are alive: the session (which keeps the
+    # transport alive) first, then the transport (ncclCommDestroy), then the torch group
     del sess
+    transport = None
+    import gc
+    gc.collect()
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
