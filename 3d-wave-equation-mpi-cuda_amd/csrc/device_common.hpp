@@ -224,12 +224,14 @@ template <class T, int AUX = 0>
 __device__ __forceinline__ T bld(__amdgpu_buffer_rsrc_t r, unsigned off) {
     return bload<AUX>((T*)nullptr, r, off);
 }
+template <int AUX = 0>
 __device__ __forceinline__ void bst(double v, __amdgpu_buffer_rsrc_t r, unsigned off) {
     using V2 = decltype(__builtin_amdgcn_raw_buffer_load_b64(r, 0, 0, 0));
-    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(V2, v), r, off, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(V2, v), r, off, 0, AUX);
 }
+template <int AUX = 0>
 __device__ __forceinline__ void bst(float v, __amdgpu_buffer_rsrc_t r, unsigned off) {
-    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), r, off, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), r, off, 0, AUX);
 }
 
 }  // namespace

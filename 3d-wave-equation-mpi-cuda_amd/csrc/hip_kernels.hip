@@ -155,7 +155,7 @@ __global__ void __launch_bounds__(kThreads) k_march(const StepParams<T> p) {
         hrow = 1 + rr;
         hcol = side ? kTK + 1 : 0;
     }
-    constexpr int kU2Aux = NT ? 2 : 0;  // non-temporal u^{n-2} (read once)
+    constexpr int kU2Aux = NT ? 2 : 0;  // non-temporal u^{n-2} (read once) and stores
 
     // slots: u1(x) -> (x - ib + 1) & 3, u2(x), halo(x), LDS buffer -> (x - ib) & 1
     V u1[4][NV], u2[2][NV];
@@ -245,13 +245,13 @@ __global__ void __launch_bounds__(kThreads) k_march(const StepParams<T> p) {
         {
             const auto rs = prs(p.u, i);
 #pragma unroll
-            for (int r = 0; r < R; ++r) bst(vget<L>(vv[r / L], r % L), rs, os[r]);
+            for (int r = 0; r < R; ++r) bst<kU2Aux>(vget<L>(vv[r / L], r % L), rs, os[r]);
 #pragma unroll
             for (int g = 0; g < 2; ++g)
                 if (i >= p.w_lo[g] && i <= p.w_hi[g]) {
                     const auto rw = prs(p.u, i + p.w_sh[g]);
 #pragma unroll
-                    for (int r = 0; r < R; ++r) bst(vget<L>(vv[r / L], r % L), rw, os[r]);
+                    for (int r = 0; r < R; ++r) bst<kU2Aux>(vget<L>(vv[r / L], r % L), rw, os[r]);
                 }
         }
         const V f0 = vsplat<L, V>(sx);

@@ -69,12 +69,16 @@ struct TbParams {
 // an in-flight register (the rotate-by-copy form serialised every plane on load latency).
 // ABL (measurement ablation, env WAVE3D_TB_ABLATION, not a solver mode): 1 = no error
 // reduction at all, 2 = absolute error only (no relative-error division).
-template <class T, bool FIRST, int R, int NW, int WPE = 1, int ABL = 0>
+// C and D are written with the non-temporal policy (+3-5 % at N=512,
+// profiles/sweep_tb2_cache_policy_r1.txt). OPT (env WAVE3D_TB_OPT, A/B ablation, bitwise-
+// neutral): 1 = default-policy stores instead.
+template <class T, bool FIRST, int R, int NW, int WPE = 1, int ABL = 0, int OPT = 0>
 __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WPE, 8))) k_tb2(const TbParams<T> p) {
     constexpr int TJ = NW * R;
     constexpr int AH = TJ + 4, AW = kTK + 4;  // A tile: rows jt-2..jt+TJ+1, cols kb-2..kb+65
     constexpr int CH = TJ + 2, CW = kTK + 2;  // C tile: rows jt-1..jt+TJ,   cols kb-1..kb+64
     constexpr unsigned ES = sizeof(T);
+    constexpr int kStAux = OPT == 1 ? 0 : 2;  // store cache policy: 2 = non-temporal
     static_assert(128 + 2 * CH <= NW * 64 && 132 + 2 * CH <= NW * 64, "ring needs more lanes");
     __shared__ T ldsA[2][AH][AW];
     __shared__ T ldsC[2][CH][CW];
@@ -265,13 +269,13 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WP
         if (i >= ib && i <= ie) {
             const auto rc = prs(p.C, i);
 #pragma unroll
-            for (int r = 0; r < R; ++r) bst(c[S0][r], rc, os[r]);
+            for (int r = 0; r < R; ++r) bst<kStAux>(c[S0][r], rc, os[r]);
 #pragma unroll
             for (int g = 0; g < 2; ++g)
                 if (i >= p.wc_lo[g] && i <= p.wc_hi[g]) {
                     const auto rw = prs(p.C, i + p.wc_sh[g]);
 #pragma unroll
-                    for (int r = 0; r < R; ++r) bst(c[S0][r], rw, os[r]);
+                    for (int r = 0; r < R; ++r) bst<kStAux>(c[S0][r], rw, os[r]);
                 }
             const bool erow = i >= p.ei0 && i <= p.ei1;
             const T sx = ldconst(p.tx, i);
@@ -304,13 +308,13 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WP
             }
             const auto rd = prs(p.D, id);
 #pragma unroll
-            for (int r = 0; r < R; ++r) bst(dv[r], rd, os[r]);
+            for (int r = 0; r < R; ++r) bst<kStAux>(dv[r], rd, os[r]);
 #pragma unroll
             for (int g = 0; g < 2; ++g)
                 if (id >= p.wd_lo[g] && id <= p.wd_hi[g]) {
                     const auto rw = prs(p.D, id + p.wd_sh[g]);
 #pragma unroll
-                    for (int r = 0; r < R; ++r) bst(dv[r], rw, os[r]);
+                    for (int r = 0; r < R; ++r) bst<kStAux>(dv[r], rw, os[r]);
                 }
             const bool erow = id >= p.ei0 && id <= p.ei1;
             const T sx = ldconst(p.tx, id);
@@ -364,8 +368,13 @@ static void (*tb_kernel(int rows, int waves, int occ))(const TbParams<T>) {
                 const char* e = std::getenv("WAVE3D_TB_ABLATION");
                 return e ? std::atoi(e) : 0;
             }();
+            static const int opt = [] {
+                const char* e = std::getenv("WAVE3D_TB_OPT");
+                return e ? std::atoi(e) : 0;
+            }();
             if (abl == 1) return k_tb2<T, F, 2, 4, 1, 1>;
             if (abl == 2) return k_tb2<T, F, 2, 4, 1, 2>;
+            if (opt == 1) return k_tb2<T, F, 2, 4, 1, 0, 1>;
             return k_tb2<T, F, 2, 4>;
         }
         case 2044: return k_tb2<T, F, 2, 4, 4>;

@@ -321,13 +321,13 @@ __global__ void __launch_bounds__(NW * 64) k_tb3(const Tb3Params<T> p) {
             if (id >= ib && id <= ie) {
                 const auto rd = prs(p.D, id);
 #pragma unroll
-                for (int r = 0; r < R; ++r) bst(d[S0][r], rd, os[r]);
+                for (int r = 0; r < R; ++r) bst<2>(d[S0][r], rd, os[r]);
 #pragma unroll
                 for (int g = 0; g < 2; ++g)
                     if (id >= p.wd_lo[g] && id <= p.wd_hi[g]) {
                         const auto rw = prs(p.D, id + p.wd_sh[g]);
 #pragma unroll
-                        for (int r = 0; r < R; ++r) bst(d[S0][r], rw, os[r]);
+                        for (int r = 0; r < R; ++r) bst<2>(d[S0][r], rw, os[r]);
                     }
                 const bool erow = id >= p.ei0 && id <= p.ei1;
                 const T sx = ldconst(p.tx, id);
@@ -354,13 +354,13 @@ __global__ void __launch_bounds__(NW * 64) k_tb3(const Tb3Params<T> p) {
             }
             const auto re = prs(p.E, ie2);
 #pragma unroll
-            for (int r = 0; r < R; ++r) bst(ev[r], re, os[r]);
+            for (int r = 0; r < R; ++r) bst<2>(ev[r], re, os[r]);
 #pragma unroll
             for (int g = 0; g < 2; ++g)
                 if (ie2 >= p.we_lo[g] && ie2 <= p.we_hi[g]) {
                     const auto rw = prs(p.E, ie2 + p.we_sh[g]);
 #pragma unroll
-                    for (int r = 0; r < R; ++r) bst(ev[r], rw, os[r]);
+                    for (int r = 0; r < R; ++r) bst<2>(ev[r], rw, os[r]);
                 }
             const bool erow = ie2 >= p.ei0 && ie2 <= p.ei1;
             const T sx = ldconst(p.tx, ie2);
