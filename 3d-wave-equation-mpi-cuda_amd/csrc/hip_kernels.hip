@@ -155,7 +155,8 @@ __global__ void __launch_bounds__(kThreads) k_march(const StepParams<T> p) {
         hrow = 1 + rr;
         hcol = side ? kTK + 1 : 0;
     }
-    constexpr int kU2Aux = NT ? 2 : 0;  // non-temporal u^{n-2} (read once) and stores
+    constexpr int kU2Aux = NT ? 2 : 0;  // non-temporal u^{n-2} (read once)
+    constexpr int kStAux = 2;           // non-temporal stores (write-once stream)
 
     // slots: u1(x) -> (x - ib + 1) & 3, u2(x), halo(x), LDS buffer -> (x - ib) & 1
     V u1[4][NV], u2[2][NV];
@@ -245,13 +246,13 @@ __global__ void __launch_bounds__(kThreads) k_march(const StepParams<T> p) {
         {
             const auto rs = prs(p.u, i);
 #pragma unroll
-            for (int r = 0; r < R; ++r) bst<kU2Aux>(vget<L>(vv[r / L], r % L), rs, os[r]);
+            for (int r = 0; r < R; ++r) bst<kStAux>(vget<L>(vv[r / L], r % L), rs, os[r]);
 #pragma unroll
             for (int g = 0; g < 2; ++g)
                 if (i >= p.w_lo[g] && i <= p.w_hi[g]) {
                     const auto rw = prs(p.u, i + p.w_sh[g]);
 #pragma unroll
-                    for (int r = 0; r < R; ++r) bst<kU2Aux>(vget<L>(vv[r / L], r % L), rw, os[r]);
+                    for (int r = 0; r < R; ++r) bst<kStAux>(vget<L>(vv[r / L], r % L), rw, os[r]);
                 }
         }
         const V f0 = vsplat<L, V>(sx);
@@ -488,7 +489,8 @@ KernelVariant parse_kernel_variant(const std::string& name) {
         return v;
     }
     if (name == "auto") {  // best measured single-step variant on MI355X (profiles/)
-        v.rows = 2;
+        v.rows = 4;  // march4nt: 231 Gpts/s fp64 at N=512 (profiles/sweep_store_policy_r1.txt)
+        v.nt = true;
         return v;
     }
     W3D_REQUIRE(name.rfind("march", 0) == 0, "wave3d: unknown kernel variant " + name);

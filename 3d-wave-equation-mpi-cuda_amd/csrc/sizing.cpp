@@ -38,6 +38,8 @@ Layout plan_layout(const Config& c, int world) {
     l.tb = auto_tb || tb3 || c.kernel.rfind("tb2", 0) == 0;
     l.depth = tb3 ? 3 : (l.tb ? 2 : 1);
     if (tb3) l.rows = 2, l.waves = 8;  // measured best three-layer tile (profiles/)
+    // fp32: 16-row tiles (tb2r4, 95 VGPRs) beat 8-row ones by ~4 % at N=512
+    if (auto_tb && c.dtype == DType::F32) l.rows = 4;
     if (l.tb && !auto_tb) parse_tb(c.kernel, l.rows, l.waves, l.occ);
     l.G = l.depth;      // ghost depth = layers per sweep
     l.L = l.depth + 2;  // 3 / 4 / 5 time levels (tb3: C never stored, D and E written)
