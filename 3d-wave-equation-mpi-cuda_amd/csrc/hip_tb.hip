@@ -71,14 +71,15 @@ struct TbParams {
 // reduction at all, 2 = absolute error only (no relative-error division).
 // C and D are written with the non-temporal policy (+3-5 % at N=512,
 // profiles/sweep_tb2_cache_policy_r1.txt). OPT (env WAVE3D_TB_OPT, A/B ablation, bitwise-
-// neutral): 1 = default-policy stores instead.
+// neutral): 1 = default-policy stores instead. (Prefetch distances: own A and both A rings 2
+// planes, B 1 plane; B at distance 2 measured no faster, the outer ring at distance 2 +2.6 %.)
 template <class T, bool FIRST, int R, int NW, int WPE = 1, int ABL = 0, int OPT = 0>
 __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WPE, 8))) k_tb2(const TbParams<T> p) {
     constexpr int TJ = NW * R;
     constexpr int AH = TJ + 4, AW = kTK + 4;  // A tile: rows jt-2..jt+TJ+1, cols kb-2..kb+65
     constexpr int CH = TJ + 2, CW = kTK + 2;  // C tile: rows jt-1..jt+TJ,   cols kb-1..kb+64
     constexpr unsigned ES = sizeof(T);
-    constexpr int kStAux = OPT == 1 ? 0 : 2;  // store cache policy: 2 = non-temporal
+    constexpr int kStAux = (OPT & 1) ? 0 : 2;  // store cache policy: 2 = non-temporal
     static_assert(128 + 2 * CH <= NW * 64 && 132 + 2 * CH <= NW * 64, "ring needs more lanes");
     __shared__ T ldsA[2][AH][AW];
     __shared__ T ldsC[2][CH][CW];
@@ -153,11 +154,12 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WP
     const unsigned ua_off = boff(uj, uk, uon && inb(uj, uk));
 
     // Slots (iteration i = ib - 1 + q, phase P = q & 3):
-    //   A(x), ring A(x): slot (x - ib + 2) & 3 -> A(i-1) = P, A(i) = P+1, A(i+1) = P+2, A(i+2) = P+3
+    //   A(x), ring A(x), outer A(x): slot (x - ib + 2) & 3 -> A(i-1) = P, A(i) = P+1,
+    //                                 A(i+1) = P+2, A(i+2) = P+3
     //   C(x):            slot (x - ib + 1) & 3 -> C(i) = P, C(i-1) = P+3, C(i-2) = P+2
-    //   B(x), ring B(x), outer A(x), LDS buffer: (x - ib + 1) & 1
+    //   B(x), ring B(x), LDS buffer: (x - ib + 1) & 1
     T a[4][R], c[4][R], bb[2][R];
-    T ra[4], rb[2], ua[2];
+    T ra[4], rb[2], ua[4];
     {
         const auto r0 = prs(p.A, ib - 2), r1 = prs(p.A, ib - 1), r2 = prs(p.A, ib);
         const auto rB = prs(p.B, ib - 1);
@@ -178,15 +180,16 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WP
         ra[3] = T(0);
         rb[0] = bld<T>(rB, rb_off);
         rb[1] = T(0);
-        ua[0] = bld<T>(r1, ua_off);
-        ua[1] = T(0);
+        ua[0] = ua[3] = T(0);
+        ua[1] = bld<T>(r1, ua_off);
+        ua[2] = bld<T>(r2, ua_off);
     }
 
     T ma1 = T(kErrInit), ma2 = T(kErrInit);
     RelArg<T> mr1, mr2;
     bool bad1 = false, bad2 = false;
 
-    // prefetch A(i+2) (own, ring), A(i+1) (outer ring), B(i+1); on the last plane the
+    // prefetch A(i+2) (own, both rings), B(i+1); on the last plane the
     // descriptors get 0 records, so the loads return 0 without touching memory (uniform,
     // no per-lane masking)
     auto prefetch = [&](auto phase, const int i) {
@@ -196,7 +199,6 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WP
         const unsigned nb = more ? pbytes : 0u;
         const int d2 = more ? 2 : 0, d1 = more ? 1 : 0;
         const auto rA2 = plane_rsrc(p.A + (i64(i + d2) * si - p.poff), nb);
-        const auto rA1 = plane_rsrc(p.A + (i64(i + d1) * si - p.poff), nb);
         const auto rB1 = plane_rsrc(p.B + (i64(i + d1) * si - p.poff), nb);
 #pragma unroll
         for (int r = 0; r < R; ++r) {
@@ -205,7 +207,7 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WP
         }
         ra[S3] = bld<T>(rA2, ra_off);
         rb[H1] = bld<T>(rB1, rb_off);
-        ua[H1] = bld<T>(rA1, ua_off);
+        ua[S3] = bld<T>(rA2, ua_off);
     };
 
     // stage A(i) (own from registers, rings from the prefetch) into LDS buffer (i - ib + 1) & 1
@@ -215,7 +217,7 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WP
 #pragma unroll
         for (int r = 0; r < R; ++r) ldsA[H0][2 + w * R + r][2 + lane] = a[S1][r];
         if (ron) ldsA[H0][rj - jt + 2][rk - kb + 2] = ra[S1];
-        if (uon) ldsA[H0][uj - jt + 2][uk - kb + 2] = ua[H0];
+        if (uon) ldsA[H0][uj - jt + 2][uk - kb + 2] = ua[S1];
     };
 
     // C(i) and D(i-1). ALIAS: this plane is a periodic seam, where C(i)'s x+ / x- neighbour
