@@ -217,7 +217,12 @@ private:
         auto tabx = prob_.table_x(), taby = prob_.table_y(), tabz = prob_.table_z();
         ct_ = prob_.table_t();
         HIP_CHECK(hipStreamCreateWithFlags(&s_comp_, hipStreamNonBlocking));
-        HIP_CHECK(hipStreamCreateWithFlags(&s_comm_, hipStreamNonBlocking));
+        // the halo stream (pack/unpack, RCCL kernels) at the highest priority, so its small
+        // launches are dispatched ahead of the interior sweep's queued workgroups instead of
+        // waiting for CU slots behind them
+        int prio_lo = 0, prio_hi = 0;
+        HIP_CHECK(hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi));
+        HIP_CHECK(hipStreamCreateWithPriority(&s_comm_, hipStreamNonBlocking, prio_hi));
         HIP_CHECK(hipEventCreateWithFlags(&ev_start_, hipEventDefault));
         HIP_CHECK(hipEventCreateWithFlags(&ev_end_, hipEventDefault));
         HIP_CHECK(hipEventCreateWithFlags(&ev_layer_, hipEventDisableTiming));
