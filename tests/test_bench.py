@@ -1,0 +1,70 @@
+"""bench.py output contract: one JSON line with the driver's fields, the BASELINE.json metric,
+and an L-inf that equals the reference golden for the config it ran."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+FIELDS = {"metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
+          "scaling", "vs_baseline", "dtype", "data", "config"}
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _bench(extra, nproc=1, timeout=300):
+    if nproc == 1:
+        cmd = [sys.executable, os.path.join(ROOT, "bench.py")] + extra
+    else:
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
+               "--master-addr", "127.0.0.1", "--master-port", str(_port()),
+               os.path.join(ROOT, "bench.py"), "--gpus", str(nproc)] + extra
+    out = subprocess.run(cmd, capture_output=True, text=True, cwd=ROOT, timeout=timeout)
+    assert out.returncode == 0, out.stderr[-2000:]
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out.stdout[-2000:]
+    return json.loads(lines[0])
+
+
+def _check(r, n, steps, warmup):
+    with open(os.path.join(ROOT, "BASELINE.json")) as f:
+        metric = json.load(f)["metric"]
+    assert FIELDS <= set(r)
+    assert r["metric"] == metric and r["unit"] == "Mpoints/s" and r["higher_is_better"] is True
+    assert r["n_gpus"] == n and r["steps"] == steps and r["warmup"] == warmup
+    assert r["value"] > 0 and r["ms_per_step"] > 0 and r["dtype"] == "fp64"
+    cfg = r["config"]
+    pts = (cfg["N"] + 1) ** 3 * cfg["timesteps"]
+    # value = whole-job points per second over the timed solves (ms_per_step is one solve)
+    assert r["value"] == pytest.approx(pts / (r["ms_per_step"] * 1e3), rel=1e-3)
+
+
+def test_bench_cpu_single_process():
+    r = _bench(["--backend", "cpu", "--N", "32", "--timesteps", "20", "--steps", "1", "--warmup", "0"])
+    _check(r, 1, 1, 0)
+    assert f"{r['linf_abs']:.6g}" == "0.000175963"  # golden N=32 K=20
+
+
+def test_bench_cpu_two_ranks_gloo():
+    r = _bench(["--backend", "cpu", "--N", "32", "--timesteps", "20", "--steps", "1", "--warmup", "0"],
+               nproc=2)
+    _check(r, 2, 1, 0)
+    assert r["scaling"] == "strong"  # global N fixed by --N
+    assert f"{r['linf_abs']:.6g}" == "0.000175963"
+
+
+@pytest.mark.gpu
+def test_bench_gpu_default_config_short():
+    r = _bench(["--steps", "1", "--warmup", "1"])
+    _check(r, 1, 1, 1)
+    assert r["scaling"] == "weak" and r["config"]["N"] == 512 and r["config"]["timesteps"] == 100
+    assert f"{r['linf_abs']:.6g}" == "6.03381e-07"  # golden N=512 K=100
