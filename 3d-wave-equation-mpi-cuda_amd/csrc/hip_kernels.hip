@@ -647,7 +647,7 @@ void launch_init(T* u, const GridView& gv, const Box& bx, const Wrap& wrap, cons
                 "init box outside the owned region");
     const int planes = bx.i1 - bx.i0 + 1;
     const int tiles = cdiv(bx.k1 - bx.k0 + 1, 64) * cdiv(bx.j1 - bx.j0 + 1, kWaves);
-    const int chunk = std::min(planes, std::max(1, cdiv(planes * tiles, 4096 * 4)));
+    const int chunk = std::min(planes, std::max(1, cdiv(planes * tiles, 4096)));
     dim3 grid(cdiv(bx.k1 - bx.k0 + 1, 64), cdiv(bx.j1 - bx.j0 + 1, kWaves), cdiv(planes, chunk));
     hipLaunchKernelGGL(k_init<T>, grid, dim3(kThreads), 0, s, u, gv.si, gv.sj, bx, chunk, wrap, tx,
                        ty, tz, T(ct0), err);
