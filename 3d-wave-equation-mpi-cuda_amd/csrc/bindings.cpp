@@ -88,6 +88,8 @@ py::dict result_dict(const Config& c, const RunResult& r) {
     d["layers_done"] = r.layers_done;
     d["resumed_from"] = r.resumed_from;
     d["graph"] = r.graph;
+    d["overlap"] = r.overlap;
+    d["comm_size"] = r.comm_size;
     d["report"] = format_report(c, r);
     d["output_file"] = output_filename(c, r);
     d["json"] = json_summary(c, r);
@@ -205,7 +207,8 @@ PYBIND11_MODULE(_wave3d_C, m) {
             py::gil_scoped_release nogil;
             t.barrier();
         })
-        .def("check_async", &RcclTransport::check_async);
+        .def("check_async", &RcclTransport::check_async)
+        .def("comm_size", &RcclTransport::comm_size);
     m.def("rccl_unique_id", []() { return py::bytes(rccl_unique_id()); });
 
     py::class_<Session>(m, "Session", "Persistent solver: allocate once, solve() many times")
@@ -315,6 +318,8 @@ PYBIND11_MODULE(_wave3d_C, m) {
         Topology::dims_create(n, d);
         return std::vector<int>{d[0], d[1], d[2]};
     });
+    m.def("checkpoint_layers", &checkpoint_layers, py::arg("dir"), py::arg("rank"),
+          "Layers with a complete checkpoint file of `rank` in `dir` (ascending).");
     m.def("encode_max_key", &encode_max_key);
     m.def("decode_max_key", &decode_max_key);
     m.def("march_rows_per_thread", &march_rows_per_thread);

@@ -1,8 +1,16 @@
 #include "checkpoint.hpp"
 
+#include <dirent.h>
+#include <fcntl.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <cerrno>
 #include <cstdio>
 #include <cstring>
 #include <fstream>
+#include <functional>
 
 namespace wave3d {
 
@@ -28,21 +36,42 @@ CheckpointHeader make_header(const Config& c, const Topology& t, int layer, int 
     return h;
 }
 
-std::string checkpoint_path(const std::string& dir, int rank) {
-    return dir + "/ckpt_r" + std::to_string(rank) + ".bin";
+std::string checkpoint_path(const std::string& dir, int rank, int layer) {
+    return dir + "/ckpt_r" + std::to_string(rank) + "_L" + std::to_string(layer) + ".bin";
 }
 
 namespace {
 
-void io_owned(std::fstream& f, const HostLevel& L, int es, bool write) {
+void io_owned(const HostLevel& L, int es, const std::function<void(char*, size_t)>& op) {
     const size_t row = size_t(L.Z) * es;
     char* base = static_cast<char*>(L.origin);
     for (int i = 1; i <= L.X; ++i)
-        for (int j = 1; j <= L.Y; ++j) {
-            char* p = base + (size_t(i) * L.si + size_t(j) * L.sj + 1) * es;
-            if (write) f.write(p, row);
-            else f.read(p, row);
-        }
+        for (int j = 1; j <= L.Y; ++j) op(base + (size_t(i) * L.si + size_t(j) * L.sj + 1) * es, row);
+}
+
+void write_all(int fd, const void* p, size_t n, const std::string& path) {
+    const char* c = static_cast<const char*>(p);
+    while (n > 0) {
+        const ssize_t w = ::write(fd, c, n);
+        if (w < 0 && errno == EINTR) continue;
+        W3D_REQUIRE(w > 0, "checkpoint write failed " + path + ": " + std::strerror(errno));
+        c += w, n -= size_t(w);
+    }
+}
+
+void fsync_dir(const std::string& dir) {
+    const int fd = ::open(dir.c_str(), O_RDONLY | O_DIRECTORY);
+    if (fd >= 0) {
+        (void)::fsync(fd);
+        ::close(fd);
+    }
+}
+
+bool read_header(const std::string& path, CheckpointHeader& h) {
+    std::ifstream f(path, std::ios::binary);
+    if (!f.good()) return false;
+    f.read(reinterpret_cast<char*>(&h), sizeof(h));
+    return f.good() && std::memcmp(h.magic, CheckpointHeader().magic, 8) == 0;
 }
 
 }  // namespace
@@ -50,38 +79,80 @@ void io_owned(std::fstream& f, const HostLevel& L, int es, bool write) {
 void write_checkpoint(const std::string& dir, const CheckpointHeader& h, const HostLevel& prev,
                       const HostLevel& cur, const std::vector<double>& max_abs,
                       const std::vector<double>& max_rel) {
-    std::string path = checkpoint_path(dir, h.rank);
-    std::string tmp = path + ".tmp";
-    {
-        std::fstream f(tmp, std::ios::out | std::ios::binary | std::ios::trunc);
-        W3D_REQUIRE(f.good(), "cannot write checkpoint " + tmp);
-        f.write(reinterpret_cast<const char*>(&h), sizeof(h));
-        int n = h.layer + 1;
-        f.write(reinterpret_cast<const char*>(max_abs.data()), sizeof(double) * n);
-        f.write(reinterpret_cast<const char*>(max_rel.data()), sizeof(double) * n);
-        io_owned(f, prev, h.elem_size, true);
-        io_owned(f, cur, h.elem_size, true);
-        W3D_REQUIRE(f.good(), "checkpoint write failed " + tmp);
+    const std::string path = checkpoint_path(dir, h.rank, h.layer);
+    const std::string tmp = path + ".tmp";
+    const int fd = ::open(tmp.c_str(), O_WRONLY | O_CREAT | O_TRUNC, 0644);
+    W3D_REQUIRE(fd >= 0, "cannot write checkpoint " + tmp + ": " + std::strerror(errno));
+    try {
+        write_all(fd, &h, sizeof(h), tmp);
+        const size_t n = size_t(h.layer) + 1;
+        write_all(fd, max_abs.data(), sizeof(double) * n, tmp);
+        write_all(fd, max_rel.data(), sizeof(double) * n, tmp);
+        auto w = [&](char* p, size_t b) { write_all(fd, p, b, tmp); };
+        io_owned(prev, h.elem_size, w);
+        io_owned(cur, h.elem_size, w);
+        W3D_REQUIRE(::fsync(fd) == 0, "fsync failed on " + tmp);
+    } catch (...) {
+        ::close(fd);
+        throw;
     }
+    ::close(fd);
     W3D_REQUIRE(std::rename(tmp.c_str(), path.c_str()) == 0, "cannot rename " + tmp);
+    fsync_dir(dir);
 }
 
-int checkpoint_layer(const std::string& dir, int rank) {
-    std::string path = checkpoint_path(dir, rank);
-    std::fstream f(path, std::ios::in | std::ios::binary);
-    W3D_REQUIRE(f.good(), "cannot open checkpoint " + path);
-    CheckpointHeader h;
-    f.read(reinterpret_cast<char*>(&h), sizeof(h));
-    W3D_REQUIRE(f.good() && std::memcmp(h.magic, CheckpointHeader().magic, 8) == 0,
-                "not a checkpoint: " + path);
-    return h.layer;
+std::vector<int> checkpoint_layers(const std::string& dir, int rank) {
+    std::vector<int> out;
+    DIR* d = ::opendir(dir.c_str());
+    if (!d) return out;
+    const std::string pre = "ckpt_r" + std::to_string(rank) + "_L";
+    while (dirent* e = ::readdir(d)) {
+        const std::string name = e->d_name;
+        if (name.rfind(pre, 0) != 0 || name.size() < pre.size() + 5) continue;
+        if (name.compare(name.size() - 4, 4, ".bin") != 0) continue;  // skips *.bin.tmp
+        const std::string num = name.substr(pre.size(), name.size() - pre.size() - 4);
+        if (num.empty() || num.find_first_not_of("0123456789") != std::string::npos) continue;
+        CheckpointHeader h;
+        const int layer = std::stoi(num);
+        if (read_header(dir + "/" + name, h) && h.layer == layer && h.rank == rank) out.push_back(layer);
+    }
+    ::closedir(d);
+    std::sort(out.begin(), out.end());
+    return out;
+}
+
+void prune_checkpoints(const std::string& dir, int rank, int keep) {
+    const std::vector<int> l = checkpoint_layers(dir, rank);
+    for (size_t q = 0; q + size_t(keep) < l.size(); ++q)
+        (void)std::remove(checkpoint_path(dir, rank, l[q]).c_str());
+}
+
+int agree_resume_layer(const std::string& dir, const std::vector<int>& local_ranks, Transport* ext) {
+    // newest layer complete on every local rank (ranks keep two generations, see header)
+    double neg = -1e300;  // max over ranks of -(newest common layer) = -(min)
+    for (int r : local_ranks) {
+        const std::vector<int> l = checkpoint_layers(dir, r);
+        W3D_REQUIRE(!l.empty(), "no checkpoint of rank " + std::to_string(r) + " in " + dir);
+        neg = std::max(neg, -double(l.back()));
+    }
+    if (ext) ext->allreduce_max_host(&neg, 1);
+    const int n = int(-neg);
+    double missing = 0;
+    for (int r : local_ranks) {
+        const std::vector<int> l = checkpoint_layers(dir, r);
+        if (!std::binary_search(l.begin(), l.end(), n)) missing = 1;
+    }
+    if (ext) ext->allreduce_max_host(&missing, 1);
+    W3D_REQUIRE(missing == 0, "checkpoints in " + dir + " have no layer common to every rank (newest common " +
+                                  std::to_string(n) + ")");
+    return n;
 }
 
 int read_checkpoint(const std::string& dir, const CheckpointHeader& expect, const HostLevel& prev,
                     const HostLevel& cur, std::vector<double>& max_abs,
                     std::vector<double>& max_rel) {
-    std::string path = checkpoint_path(dir, expect.rank);
-    std::fstream f(path, std::ios::in | std::ios::binary);
+    const std::string path = checkpoint_path(dir, expect.rank, expect.layer);
+    std::ifstream f(path, std::ios::binary);
     W3D_REQUIRE(f.good(), "cannot open checkpoint " + path);
     CheckpointHeader h;
     f.read(reinterpret_cast<char*>(&h), sizeof(h));
@@ -89,7 +160,7 @@ int read_checkpoint(const std::string& dir, const CheckpointHeader& expect, cons
     bool same = h.N == expect.N && h.K == expect.K && h.nprocs == expect.nprocs &&
                 h.rank == expect.rank && h.elem_size == expect.elem_size &&
                 h.pi_mode == expect.pi_mode && h.ic_mode == expect.ic_mode && h.T == expect.T &&
-                h.Lx == expect.Lx && h.Ly == expect.Ly && h.Lz == expect.Lz;
+                h.Lx == expect.Lx && h.Ly == expect.Ly && h.Lz == expect.Lz && h.layer == expect.layer;
     for (int a = 0; a < 3; ++a)
         same = same && h.dims[a] == expect.dims[a] && h.coords[a] == expect.coords[a] &&
                h.ext[a] == expect.ext[a];
@@ -100,8 +171,9 @@ int read_checkpoint(const std::string& dir, const CheckpointHeader& expect, cons
     max_rel.assign(n + 1, 0.0);
     f.read(reinterpret_cast<char*>(max_abs.data()), sizeof(double) * (n + 1));
     f.read(reinterpret_cast<char*>(max_rel.data()), sizeof(double) * (n + 1));
-    io_owned(f, prev, h.elem_size, false);
-    io_owned(f, cur, h.elem_size, false);
+    auto r = [&](char* p, size_t b) { f.read(p, std::streamsize(b)); };
+    io_owned(prev, h.elem_size, r);
+    io_owned(cur, h.elem_size, r);
     W3D_REQUIRE(f.good(), "truncated checkpoint " + path);
     return n;
 }

@@ -2,15 +2,21 @@
 //
 // State needed to resume after layer n: the two newest levels u^{n-1}, u^n (owned nodes
 // only, no ghosts), n itself, and the global per-layer error maxima for layers 0..n.
-// One file per rank, `<dir>/ckpt_r<rank>.bin`, written to a temp name then renamed so a
-// crash never leaves a torn checkpoint. The header pins N, K, the decomposition and the
-// physics so a resume with a different configuration is refused.
+// One file per rank and checkpoint layer, `<dir>/ckpt_r<rank>_L<n>.bin`, written to a temp
+// name, fsync'ed, then renamed (and the directory fsync'ed) so a crash never leaves a torn
+// file. Every rank keeps its two newest complete generations: ranks write asynchronously,
+// but the halo exchanges keep them within one checkpoint of each other, so the newest layer
+// that *every* rank has complete is always still on disk. Resume agrees on that layer across
+// all ranks (local ones and, through the transport, every process) before reading anything,
+// so processes never resume from different layers. The header pins N, K, the decomposition
+// and the physics so a resume with a different configuration is refused.
 #pragma once
 
 #include <string>
 #include <vector>
 
 #include "config.hpp"
+#include "halo.hpp"
 #include "topology.hpp"
 
 namespace wave3d {
@@ -28,7 +34,14 @@ struct CheckpointHeader {
 };
 
 CheckpointHeader make_header(const Config& c, const Topology& t, int layer, int elem_size);
-std::string checkpoint_path(const std::string& dir, int rank);
+std::string checkpoint_path(const std::string& dir, int rank, int layer);
+// Layers for which `rank` has a complete checkpoint file in `dir`, ascending.
+std::vector<int> checkpoint_layers(const std::string& dir, int rank);
+// Remove the rank's files older than its `keep` newest complete generations.
+void prune_checkpoints(const std::string& dir, int rank, int keep = 2);
+// The resume layer: newest layer for which every rank (the local ones, and every process
+// through `ext` when given) has a complete file; throws if some rank lacks it.
+int agree_resume_layer(const std::string& dir, const std::vector<int>& local_ranks, Transport* ext);
 
 // Host view of one level: element (i,j,k) of the owned block (1..X, 1..Y, 1..Z) lives at
 // origin + (i*si + j*sj + k) elements. Only owned nodes are stored.
@@ -42,10 +55,9 @@ void write_checkpoint(const std::string& dir, const CheckpointHeader& h, const H
                       const HostLevel& cur, const std::vector<double>& max_abs,
                       const std::vector<double>& max_rel);
 
-// Validates the header against `expect` (layer ignored), fills the owned nodes of `prev`
-// (u^{n-1}) and `cur` (u^n), returns n. Call checkpoint_layer() first to learn n.
+// Reads the checkpoint of expect.rank at expect.layer: validates the header against `expect`,
+// fills the owned nodes of `prev` (u^{n-1}) and `cur` (u^n), returns n.
 int read_checkpoint(const std::string& dir, const CheckpointHeader& expect, const HostLevel& prev,
                     const HostLevel& cur, std::vector<double>& max_abs, std::vector<double>& max_rel);
-int checkpoint_layer(const std::string& dir, int rank);
 
 }  // namespace wave3d

@@ -15,6 +15,8 @@ std::string usage() {
            "  --dims a,b,c           override the Cartesian process grid\n"
            "  --ranks P              simulate P ranks in-process (loopback transport)\n"
            "  --transport auto|rccl|loopback\n"
+           "  --x-self-transport     one x rank: send the periodic wrap through the transport\n"
+           "                         to this rank (exercises RCCL send/recv on a single GPU)\n"
            "  --no-overlap           no interior/shell split\n"
            "  --kernel K             auto (= tb2) | tb2[r<R>][w<W>] | tb3[r<R>w<W>] | march[2|4|8][nt|p|f]\n"
            "                         | naive | flat   (temporal blocking / single-step variants)\n"
@@ -122,6 +124,8 @@ Config parse_cli(const std::vector<std::string>& a) {
             c.ranks = parse_int(need(i++), "ranks");
         } else if (o == "--transport") {
             c.transport = need(i++);
+        } else if (o == "--x-self-transport") {
+            c.x_self_transport = true;
         } else if (o == "--no-overlap") {
             c.overlap = false;
         } else if (o == "--overlap") {

@@ -35,6 +35,9 @@ struct Config {
     int check_every = 0;            // >0: abort early when a layer's error is NaN/Inf/>1
     bool strict_cfl = false;        // refuse C > 1/sqrt(3)
     std::string transport = "auto"; // auto | rccl | loopback
+    bool x_self_transport = false;  // dims[0] == 1 with an external transport: the periodic
+                                    // x wrap travels as messages to this rank (RCCL self
+                                    // send/recv) instead of the fused local wrap (testing)
     int ranks = 0;                  // >0: number of logical ranks simulated in-process
     ReportFormat format = ReportFormat::New;
     std::string out_dir = ".";

@@ -81,6 +81,7 @@ public:
             for (int r = 0; r < world_; ++r) local_ranks_.push_back(r);
         }
         threads_ = c.threads > 0 ? c.threads : std::max(1, c.Np);
+        W3D_REQUIRE(!c.x_self_transport, "--x-self-transport is a HIP/RCCL test mode");
     }
 
     void init() {
@@ -119,6 +120,7 @@ public:
         res.backend = "cpu";
         res.kernel = "openmp";
         res.transport = ext_ ? ext_->name() : (world_ > 1 ? "loopback" : "self");
+        res.comm_size = ext_ ? ext_->comm_size() : 0;
         res.courant = prob_.courant;
         for (int a = 0; a < 3; ++a) res.dims[a] = ranks_[0].topo.dims[a];
         Timings t;
@@ -458,6 +460,7 @@ private:
             CheckpointHeader h = make_header(cfg_, R.topo, n, sizeof(T));
             write_checkpoint(cfg_.checkpoint_dir, h, host_level(R, (n + 2) % 3),
                              host_level(R, n % 3), a, r);
+            prune_checkpoints(cfg_.checkpoint_dir, R.topo.rank, 2);
         }
     }
 
@@ -473,14 +476,13 @@ private:
     }
 
     int load_checkpoints() {
-        int n = -1;
+        std::vector<int> lr;
+        for (auto& R : ranks_) lr.push_back(R.topo.rank);
+        const int n = agree_resume_layer(cfg_.resume_dir, lr, ext_);  // same layer on every rank
         for (auto& R : ranks_) {
-            CheckpointHeader h = make_header(cfg_, R.topo, 0, sizeof(T));
-            const int lay = checkpoint_layer(cfg_.resume_dir, R.topo.rank);
-            int got = read_checkpoint(cfg_.resume_dir, h, host_level(R, (lay + 2) % 3),
-                                      host_level(R, lay % 3), ckpt_abs_, ckpt_rel_);
-            W3D_REQUIRE(n < 0 || got == n, "checkpoint layers differ between ranks");
-            n = got;
+            CheckpointHeader h = make_header(cfg_, R.topo, n, sizeof(T));
+            read_checkpoint(cfg_.resume_dir, h, host_level(R, (n + 2) % 3), host_level(R, n % 3),
+                            ckpt_abs_, ckpt_rel_);
         }
         // refill ghosts of both levels with one exchange each
         Timings dummy;

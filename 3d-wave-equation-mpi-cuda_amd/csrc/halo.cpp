@@ -2,11 +2,11 @@
 
 namespace wave3d {
 
-HaloPlan make_halo_plan(const Topology& t, i64 x_plane, int row) {
+HaloPlan make_halo_plan(const Topology& t, i64 x_plane, int row, bool self_msg) {
     HaloPlan p;
     const i64 X = t.ext[0], Y = t.ext[1];
     const i64 count[3] = {x_plane, X * row, X * (Y + 2)};
-    p.self_x = t.nbr[0][0] == t.rank;
+    p.self_x = t.nbr[0][0] == t.rank && !self_msg;
     for (int a = 0; a < 3; ++a) {
         if (a == 0 && p.self_x) continue;
         // travelling +a: send from the plus face to nbr[a][1] (tag 2a+1)

@@ -11,9 +11,12 @@
 //      received in place, no pack/unpack;
 //   y: rows i=1..X of the (i,k) face, k over the full padded row -> X*pitch elements;
 //   z: i=1..X, j=0..Y+1 of the (i,j) face                       -> X*(Y+2) elements.
-// A rank that is its own x-neighbour (dims[0] == 1) wraps locally instead of messaging.
+// A rank that is its own x-neighbour (dims[0] == 1) wraps locally instead of messaging,
+// unless `self_msg` is set: then the wrap is two messages to this rank (the same plan a
+// rank of a dims[0] >= 2 ring has, both ends being itself).
 #pragma once
 
+#include <functional>
 #include <string>
 #include <vector>
 
@@ -37,7 +40,7 @@ struct HaloPlan {
 };
 
 // `x_plane` = elements of one padded (j,k) plane, `row` = elements of a y-face row.
-HaloPlan make_halo_plan(const Topology& t, i64 x_plane, int row);
+HaloPlan make_halo_plan(const Topology& t, i64 x_plane, int row, bool self_msg = false);
 
 // Description of one message for a transport.
 struct Message {
@@ -57,6 +60,9 @@ public:
     virtual int rank() const = 0;
     virtual int size() const = 0;
     virtual bool device() const = 0;
+    // Ranks of the underlying communicator as the library itself reports them (RCCL:
+    // ncclCommCount), so a run can prove which world the halos travelled in.
+    virtual int comm_size() const { return size(); }
     virtual void exchange(const std::vector<Message>& sends, const std::vector<Message>& recvs,
                           void* stream) = 0;
     // In-place max over ranks of n order-preserving error keys (see encode_max_key).
@@ -67,7 +73,11 @@ public:
     // Wait for `stream` to drain. A transport with asynchronous failure modes (RCCL) polls
     // its error state and enforces a watchdog timeout here instead of blocking forever;
     // returns false when the caller should simply synchronise the stream itself.
-    virtual bool wait_stream(void* /*stream*/) { return false; }
+    // `progress` (optional) returns a count that grows while the device makes progress (e.g.
+    // completed per-sweep events): the watchdog measures time since it last grew.
+    virtual bool wait_stream(void* /*stream*/, const std::function<long()>* /*progress*/ = nullptr) {
+        return false;
+    }
 };
 
 }  // namespace wave3d

@@ -436,6 +436,12 @@ __global__ void k_init_err(u64* err, int n) {
     if (t < n) err[t] = (t % 3 == 2) ? 0ull : enc_key(kErrInit);
 }
 
+// Timer mark: the device's constant-rate wall clock when the stream reaches this point
+// (after every earlier kernel of the stream). One lane writes one slot.
+__global__ void k_stamp(u64* ts, int slot) {
+    if (threadIdx.x == 0) ts[slot] = wall_clock64();
+}
+
 __global__ void k_encode(const double* v, u64* k, int n) {
     const int t = blockIdx.x * blockDim.x + threadIdx.x;
     if (t < n) k[t] = enc_key(v[t]);
@@ -680,6 +686,11 @@ void launch_faces(T* u, const GridView& gv, const FaceOp<T>* ops, int nops, bool
 void launch_init_err(u64* err, int layers, hipStream_t s) {
     const int n = layers * 3;
     hipLaunchKernelGGL(k_init_err, dim3(cdiv(n, 256)), dim3(256), 0, s, err, n);
+    HIP_OK(hipGetLastError());
+}
+
+void launch_stamp(u64* ts, int slot, hipStream_t s) {
+    hipLaunchKernelGGL(k_stamp, dim3(1), dim3(64), 0, s, ts, slot);
     HIP_OK(hipGetLastError());
 }
 

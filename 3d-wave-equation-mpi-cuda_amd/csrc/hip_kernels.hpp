@@ -141,6 +141,8 @@ void launch_box_copy(const BoxCopy<T>* ops, int nops, const GridView& gv, bool t
 
 // Initialise per-layer error slots: abs/rel keys = encode(-100), flag = 0.
 void launch_init_err(u64* err, int layers, hipStream_t s);
+// ts[slot] = device wall clock (hipDeviceAttributeWallClockRate kHz) in stream order
+void launch_stamp(u64* ts, int slot, hipStream_t s);
 
 // Device encode of a double into the order-preserving key (exposed for tests).
 void launch_encode_keys(const double* v, u64* k, int n, hipStream_t s);

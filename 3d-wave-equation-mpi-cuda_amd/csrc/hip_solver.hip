@@ -134,6 +134,10 @@ public:
         naive_.flat = true;  // thin overlap shells: flattened one-point-per-thread kernel
         // interior/shell split + comm stream whenever there is a remote halo to hide
         overlap_ = c.overlap && (ext_ != nullptr || world_ > 1);
+        // test mode: the periodic x wrap of a dims[0] == 1 rank goes through the transport as
+        // messages to itself (RCCL send/recv exercised on one GPU), not the fused local wrap
+        xself_ = c.x_self_transport;
+        W3D_REQUIRE(!xself_ || ext_, "--x-self-transport needs an external (e.g. RCCL) transport");
     }
 
     ~HipSolver() { release(); }
@@ -142,6 +146,21 @@ public:
         TraceRange tr("wave3d.setup");
         auto t0 = clk::now();
         setup();
+        bool halos = fault_.kind == "drop_face";
+        for (auto& R : ranks_) halos |= !R.plan.sends.empty() || tb_halo(R);
+        fine_ = cfg_.profile || halos;
+        // every mark of a solve: IC + per sweep (compute, exchange) + reduction
+        ts_cap_ = size_t(6) * (prob_.K + 4) + 16;
+        void* h = nullptr;
+        HIP_CHECK(hipHostMalloc(&h, ts_cap_ * sizeof(u64), hipHostMallocCoherent | hipHostMallocMapped));
+        ts_host_ = static_cast<u64*>(h);
+        void* d = nullptr;
+        HIP_CHECK(hipHostGetDevicePointer(&d, h, 0));
+        ts_dev_ = static_cast<u64*>(d);
+        int dev = 0, khz = 0;
+        HIP_CHECK(hipGetDevice(&dev));
+        HIP_CHECK(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev));
+        if (khz > 0) clock_khz_ = khz;
         HIP_CHECK(hipDeviceSynchronize());
         init_ms_ = std::chrono::duration<double, std::milli>(clk::now() - t0).count();
         if (log_on(LogLevel::Info)) {
@@ -173,6 +192,8 @@ public:
         res.kernel = tb_ ? tb_name(tb_rows_, tb_waves_, tb_occ_, tbd_) : kernel_variant_name(kind_);
         res.courant = prob_.courant;
         res.transport = ext_ ? ext_->name() : (world_ > 1 ? "loopback" : "self");
+        res.overlap = overlap_;
+        res.comm_size = ext_ ? ext_->comm_size() : 0;
         for (int a = 0; a < 3; ++a) res.dims[a] = ranks_[0].topo.dims[a];
         Timings t;
         solve(res, t);
@@ -261,7 +282,7 @@ private:
             R.tx = upload(tabx, X, R.topo.off[0]);
             R.ty = upload(taby, Y, R.topo.off[1]);
             R.tz = upload(tabz, Z, R.topo.off[2]);
-            R.plan = make_halo_plan(R.topo, R.gv.si, Z + 2);
+            R.plan = make_halo_plan(R.topo, R.gv.si, Z + 2, xself_);
             if (R.plan.self_x) W3D_REQUIRE(X >= 3, "periodic self-wrap needs >= 3 x planes");
             R.sbuf.assign(R.plan.sends.size(), nullptr);
             R.rbuf.assign(R.plan.recvs.size(), nullptr);
@@ -373,7 +394,8 @@ private:
         if (s_comm_) (void)hipStreamDestroy(s_comm_);
         for (auto e : {ev_start_, ev_end_, ev_layer_, ev_halo_})
             if (e) (void)hipEventDestroy(e);
-        for (auto e : prof_) (void)hipEventDestroy(e);
+        if (ts_host_) (void)hipHostFree(ts_host_);
+        ts_host_ = ts_dev_ = nullptr;
         if (gexec_) (void)hipGraphExecDestroy(gexec_);
         gexec_ = nullptr;
         s_comp_ = s_comm_ = nullptr;
@@ -449,16 +471,19 @@ private:
         const int dA = tbd_, dB = tbd_ - 1;
         if (!R.plan.self_x) {
             W3D_REQUIRE(X >= 2 * dA, "temporal blocking needs >= 2 x depth planes per rank");
-            const bool first = t.first(0), last = t.last(0);
+            // one x rank messaging itself (--x-self-transport): the seam partner planes are
+            // its own planes X and 1 (see sweep), no alias messages
+            const bool first = t.first(0) && t.dims[0] > 1, last = t.last(0) && t.dims[0] > 1;
+            const bool lastx = t.last(0), firstx = t.first(0);
             const int up = t.nbr[0][1], dn = t.nbr[0][0];
             const bool aliasB = tbd_ == 3;
-            R.tb_sends.push_back(M{up, 11, 0, last ? X - dA : X - dA + 1, dA});
+            R.tb_sends.push_back(M{up, 11, 0, lastx ? X - dA : X - dA + 1, dA});
             if (last) R.tb_sends.push_back(M{up, 12, 0, X, 1});
-            R.tb_sends.push_back(M{up, 13, 1, last ? X - dB : X - dB + 1, dB});
+            R.tb_sends.push_back(M{up, 13, 1, lastx ? X - dB : X - dB + 1, dB});
             if (last && aliasB) R.tb_sends.push_back(M{up, 14, 1, X, 1});
-            R.tb_sends.push_back(M{dn, 21, 0, first ? 2 : 1, dA});
+            R.tb_sends.push_back(M{dn, 21, 0, firstx ? 2 : 1, dA});
             if (first) R.tb_sends.push_back(M{dn, 22, 0, 1, 1});
-            R.tb_sends.push_back(M{dn, 23, 1, first ? 2 : 1, dB});
+            R.tb_sends.push_back(M{dn, 23, 1, firstx ? 2 : 1, dB});
             if (first && aliasB) R.tb_sends.push_back(M{dn, 24, 1, 1, 1});
             R.tb_recvs.push_back(M{dn, 11, 0, 1 - dA, dA});
             if (first) R.tb_recvs.push_back(M{dn, 12, 0, kAliasPlane, 1});
@@ -643,7 +668,7 @@ private:
         const T* A = R.g[lvl(m + L_ - 1)];
         const T* B = R.g[lvl(m + L_ - 2)];
         SeamAlias<T> al;
-        if (R.plan.self_x) {
+        if (R.topo.dims[0] == 1) {  // self-wrap, fused or through the transport
             al.next_i = 0;  // ghost copy of N-1 sees x=N (own plane X) as its x+ neighbour
             al.next = A + i64(R.topo.X()) * R.gv.si;
             al.prev_i = R.topo.X() + 1;  // ghost copy of 1 sees x=0 (own plane 1) as x-
@@ -679,7 +704,7 @@ private:
         };
         const T* aA = R.alias_buf ? R.alias_buf + R.plane_off : nullptr;
         const T* aB = R.alias_bufB ? R.alias_bufB + R.plane_off : nullptr;
-        if (R.plan.self_x) {
+        if (R.topo.dims[0] == 1) {
             // ghost copy of N-1 (plane 0) sees x=N (plane X); ghost copy of 1 (X+1) sees x=0
             sp.next_i = 0, sp.nA = A + X * si;
             sp.nC = add(0, A + X * si, A + (X - 1) * si, A + (X + 1) * si, B + X * si);
@@ -785,22 +810,36 @@ private:
         }
     }
 
-    void prof_mark(hipStream_t s, int slot) {
-        if (!cfg_.profile) return;
-        hipEvent_t e;
-        HIP_CHECK(hipEventCreate(&e));
-        HIP_CHECK(hipEventRecord(e, s));
-        prof_.push_back(e);
-        prof_slot_.push_back(slot);
+    // Phase timers (the reference's C26 breakdown, mpi_new.cpp:33-34,368-371, in every run):
+    // a one-lane kernel stamps the device wall clock into a pinned host array at each mark,
+    // in stream order — captured into the hipGraph like any kernel (graph-captured event
+    // records carry no timestamps on this HIP). Slots: 0/1 compute (loop), 2/3 halo exchange
+    // (comm stream when overlapped), 4/5 final error reduction. Per-sweep ("fine") marks
+    // whenever halos move; a run without any exchange gets one loop interval around the
+    // IC + time loop instead (nothing between its kernels).
+    enum MarkMode { kAlways, kFine, kCoarse };
+    void mark(hipStream_t s, int slot, MarkMode m = kFine) {
+        if ((m == kFine && !fine_) || (m == kCoarse && fine_)) return;
+        if (tn_ >= ts_cap_) return;  // capacity is sized for every mark of a solve
+        launch_stamp(ts_dev_, int(tn_), s);
+        if (tn_ < tslot_.size()) tslot_[tn_] = slot;
+        else tslot_.push_back(slot);
+        ++tn_;
+    }
+
+    // device progress for the transport watchdog: marks of this solve stamped so far
+    long progress() {
+        while (prog_seen_ < tn_ && reinterpret_cast<volatile u64*>(ts_host_)[prog_seen_] != 0)
+            ++prog_seen_;
+        return long(prog_seen_);
     }
 
     // ---- time loop --------------------------------------------------------------------
     void solve(RunResult& res, Timings& tm) {
         TraceRange tr("wave3d.solve");
         const int K = prob_.K;
-        for (auto e : prof_) (void)hipEventDestroy(e);
-        prof_.clear();
-        prof_slot_.clear();
+        prog_seen_ = 0;
+        std::fill(ts_host_, ts_host_ + ts_cap_, u64(0));
         // No per-solve clear of the levels: every cell the stencil reads is written first
         // in this solve (IC, fused wrap / halo exchange, Dirichlet faces at n <= 3); the
         // buffers are zeroed once at allocation.
@@ -813,14 +852,18 @@ private:
         if (graph_eligible() && !gexec_ && !graph_failed_) build_graph(res);  // host-only work
         HIP_CHECK(hipEventRecord(ev_start_, s_comp_));
         if (gexec_) {
-            // the whole IC + time loop as one graph launch (no per-kernel host overhead)
+            // the whole IC + time loop as one graph launch (no per-kernel host overhead); its
+            // timer marks were captured with it
+            tn_ = graph_tn_;
             HIP_CHECK(hipGraphLaunch(gexec_, s_comp_));
             res.layers_done = K;
         } else {
+            tn_ = 0;
             int start = 1;
             if (!cfg_.resume_dir.empty()) {
                 start = load_checkpoints() + 1;
                 res.resumed_from = start - 1;
+                mark(s_comp_, 0, kCoarse);
             } else {
                 enqueue_ic();
             }
@@ -830,7 +873,7 @@ private:
 
         // final max-reduction of the per-layer slots (mpi_new.cpp:358-361)
         TraceRange trr("wave3d.reduce");
-        prof_mark(s_comp_, 4);
+        mark(s_comp_, 4, kAlways);
         const size_t nslot = size_t(K + 1) * kSlotsPerLayer;
         std::vector<u64> acc(nslot, 0);
         if (ext_) {
@@ -843,7 +886,7 @@ private:
             sync(s_comp_);
             for (size_t q = 0; q < nslot; ++q) acc[q] = std::max(acc[q], host_err_[q]);
         }
-        prof_mark(s_comp_, 5);
+        mark(s_comp_, 5, kAlways);
         HIP_CHECK(hipEventRecord(ev_end_, s_comp_));
         HIP_CHECK(hipEventSynchronize(ev_end_));
         finish_checkpoint();  // files complete when solve() returns
@@ -859,20 +902,19 @@ private:
         if (res.resumed_from >= 0)
             for (int n = 0; n <= res.resumed_from && n < int(ckpt_abs_.size()); ++n)
                 res.max_abs[n] = ckpt_abs_[n], res.max_rel[n] = ckpt_rel_[n];
-        if (cfg_.profile) collect_profile(tm);
-        else tm.loop_ms = tm.total_ms;
+        collect_profile(tm);
     }
 
     // ---- time loop ----------------------------------------------------------------------
     void enqueue_ic() {
         TraceRange tr("wave3d.ic");
-        prof_mark(s_comp_, 0);
+        mark(s_comp_, 0, kAlways);
         for (auto& R : ranks_) {
             launch_init<T>(R.g[0], R.gv, R.owned, wrap_depth(R, G_), R.tx, R.ty, R.tz, ct_[0],
                            R.err, s_comp_);
             pack_faces(R, 0, s_comp_, true);
         }
-        prof_mark(s_comp_, 1);
+        mark(s_comp_, 1);
         if (prob_.K >= 1) issue_exchange(0);
     }
 
@@ -889,7 +931,7 @@ private:
             for (int q = n; q < n + span; ++q) guard_checkpoint_level(lvl(q), s_comp_);
             if (cfg_.print_layers && !cfg_.quiet && ranks_[0].topo.rank == 0)
                 for (int q = n; q < n + span; ++q) std::cout << "calculating layer " << q << "\n";
-            prof_mark(s_comp_, 0);
+            mark(s_comp_, 0);
             for (int q = n; q < n + span; ++q)
                 for (auto& R : ranks_)
                     if (q <= L_ || q == start)
@@ -936,7 +978,7 @@ private:
             for (int q = n; q < n + span; ++q)
                 for (auto& R : ranks_)  // tb3 never stores C = u^n: a fault there goes to u^{n+1}
                     if (!(span == 3 && q == n)) inject_after_compute(R, q, s_comp_, q == n + 1 && span == 3 ? n : q);
-            prof_mark(s_comp_, 1);
+            mark(s_comp_, 1);
             const int last = n + span - 1;
             if (last < K) issue_exchange(last);
             done = last;
@@ -950,6 +992,7 @@ private:
             if (ck && last < K) save_checkpoints(last);
             n += span;
         }
+        mark(s_comp_, 1, kCoarse);
         return done;
     }
 
@@ -960,7 +1003,7 @@ private:
     // faults); a failed capture falls back to direct launches.
     bool graph_eligible() const {
         return cfg_.graph != 0 && !ext_ && cfg_.check_every == 0 && cfg_.checkpoint_every == 0 &&
-               cfg_.resume_dir.empty() && !cfg_.profile && fault_.kind.empty() &&
+               cfg_.resume_dir.empty() && fault_.kind.empty() &&
                !cfg_.print_layers;
     }
 
@@ -969,8 +1012,10 @@ private:
         hipGraph_t g = nullptr;
         try {
             HIP_CHECK(hipStreamBeginCapture(s_comp_, hipStreamCaptureModeThreadLocal));
+            tn_ = 0;
             enqueue_ic();
             enqueue_layers(res, 1);
+            graph_tn_ = tn_;
             HIP_CHECK(hipStreamEndCapture(s_comp_, &g));
             HIP_CHECK(hipGraphInstantiate(&gexec_, g, nullptr, nullptr, 0));
             HIP_CHECK(hipGraphDestroy(g));
@@ -1005,18 +1050,18 @@ private:
         if (overlap_) {
             HIP_CHECK(hipEventRecord(ev_layer_, s_comp_));
             HIP_CHECK(hipStreamWaitEvent(s_comm_, ev_layer_, 0));
-            prof_mark(s_comm_, 2);
+            mark(s_comm_, 2);
             any_exchange(n, s_comm_);
-            prof_mark(s_comm_, 3);
+            mark(s_comm_, 3);
             HIP_CHECK(hipEventRecord(ev_halo_, s_comm_));
         } else {
             bool any = false;
             for (auto& R : ranks_)
                 any |= !R.plan.sends.empty() || tb_halo(R) || fault_.kind == "drop_face";
             if (!any) return;
-            prof_mark(s_comp_, 2);
+            mark(s_comp_, 2);
             any_exchange(n, s_comp_);
-            prof_mark(s_comp_, 3);
+            mark(s_comp_, 3);
             HIP_CHECK(hipEventRecord(ev_halo_, s_comp_));
         }
     }
@@ -1024,14 +1069,12 @@ private:
     void collect_profile(Timings& tm) {
         HIP_CHECK(hipDeviceSynchronize());
         double sum[3] = {0, 0, 0};  // loop, exchange, error
-        for (size_t q = 0; q + 1 < prof_.size(); ++q) {
-            const int a = prof_slot_[q];
+        for (size_t q = 0; q + 1 < tn_; ++q) {
+            const int a = tslot_[q];
             if (a != 0 && a != 2 && a != 4) continue;
-            for (size_t r = q + 1; r < prof_.size(); ++r)
-                if (prof_slot_[r] == a + 1) {
-                    float ms = 0;
-                    HIP_CHECK(hipEventElapsedTime(&ms, prof_[q], prof_[r]));
-                    sum[a / 2] += ms;
+            for (size_t r = q + 1; r < tn_; ++r)
+                if (tslot_[r] == a + 1) {
+                    sum[a / 2] += double(i64(ts_host_[r] - ts_host_[q])) / clock_khz_;
                     break;
                 }
         }
@@ -1050,7 +1093,8 @@ private:
 
     // stream drain; with an external transport under its watchdog (RcclTransport)
     void sync(hipStream_t s) {
-        if (!(ext_ && ext_->wait_stream(s))) HIP_CHECK(hipStreamSynchronize(s));
+        const std::function<long()> prog = [this] { return progress(); };
+        if (!(ext_ && ext_->wait_stream(s, &prog))) HIP_CHECK(hipStreamSynchronize(s));
     }
 
     bool check_layer(int n, RunResult& res) {
@@ -1150,8 +1194,9 @@ private:
                 HIP_CHECK(hipEventSynchronize(ev));
                 for (size_t q = 0; q < hs.size(); ++q) {
                     write_checkpoint(dir, hs[q], lps[q], lcs[q], a, r);
+                    prune_checkpoints(dir, rk[q], 2);
                     log_msg(LogLevel::Info, "rank ", rk[q], ": checkpoint after layer ", n, " -> ",
-                            checkpoint_path(dir, rk[q]));
+                            checkpoint_path(dir, rk[q], n));
                 }
             } catch (const std::exception& e) {
                 ckpt_error_ = e.what();
@@ -1183,17 +1228,16 @@ private:
     }
 
     int load_checkpoints() {
-        int n = -1;
         HIP_CHECK(hipDeviceSynchronize());
+        std::vector<int> lr;
+        for (auto& R : ranks_) lr.push_back(R.topo.rank);
+        const int n = agree_resume_layer(cfg_.resume_dir, lr, ext_);  // same layer on every rank
         for (auto& R : ranks_) {
-            const int got_layer = checkpoint_layer(cfg_.resume_dir, R.topo.rank);
-            const int lp = lvl(got_layer + L_ - 1), lc = lvl(got_layer);
+            const int lp = lvl(n + L_ - 1), lc = lvl(n);
             std::vector<T> prev(R.elems, T(0)), cur(R.elems, T(0));
-            CheckpointHeader h = make_header(cfg_, R.topo, 0, sizeof(T));
-            int got = read_checkpoint(cfg_.resume_dir, h, host_level(R, prev, lp),
-                                      host_level(R, cur, lc), ckpt_abs_, ckpt_rel_);
-            W3D_REQUIRE(n < 0 || got == n, "checkpoint layers differ between ranks");
-            n = got;
+            CheckpointHeader h = make_header(cfg_, R.topo, n, sizeof(T));
+            read_checkpoint(cfg_.resume_dir, h, host_level(R, prev, lp), host_level(R, cur, lc),
+                            ckpt_abs_, ckpt_rel_);
             HIP_CHECK(hipMemcpy(R.alloc[lp], prev.data(), R.elems * sizeof(T), hipMemcpyHostToDevice));
             HIP_CHECK(hipMemcpy(R.alloc[lc], cur.data(), R.elems * sizeof(T), hipMemcpyHostToDevice));
             if (R.plan.self_x) {  // periodic self-wrap ghosts of both levels
@@ -1232,6 +1276,7 @@ private:
     int G_ = 1;         // ghost depth
     int L_ = 3;         // time levels kept
     bool overlap_ = false;
+    bool xself_ = false;  // --x-self-transport
     int world_ = 1;
     std::vector<int> local_;
     std::vector<DevRank<T>> ranks_;
@@ -1246,8 +1291,15 @@ private:
     std::vector<double> ckpt_abs_, ckpt_rel_;
     hipStream_t s_comp_ = nullptr, s_comm_ = nullptr;
     hipEvent_t ev_start_ = nullptr, ev_end_ = nullptr, ev_layer_ = nullptr, ev_halo_ = nullptr;
-    std::vector<hipEvent_t> prof_;
-    std::vector<int> prof_slot_;
+    u64* ts_host_ = nullptr;       // timer-mark stamps (pinned, coherent host memory)
+    u64* ts_dev_ = nullptr;        // its device address
+    size_t ts_cap_ = 0;
+    double clock_khz_ = 1e5;       // device wall-clock rate
+    std::vector<int> tslot_;       // slot of each mark, in record order
+    size_t tn_ = 0;                // marks recorded for the current solve
+    size_t graph_tn_ = 0;          // marks captured in the hipGraph
+    size_t prog_seen_ = 0;         // marks known complete (watchdog progress)
+    bool fine_ = false;            // per-sweep marks (halos move, or --profile)
     double init_ms_ = 0;
 };
 

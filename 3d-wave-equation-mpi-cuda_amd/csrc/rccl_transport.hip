@@ -75,6 +75,13 @@ void RcclTransport::exchange(const std::vector<Message>& sends, const std::vecto
     NCCL_CHECK(ncclGroupEnd());
 }
 
+int RcclTransport::comm_size() const {
+    int n = 0;
+    if (!impl_->comm) return 0;
+    NCCL_CHECK(ncclCommCount(impl_->comm, &n));
+    return n;
+}
+
 void RcclTransport::allreduce_max_u64(u64* data, size_t n, void* stream) {
     NCCL_CHECK(ncclAllReduce(data, data, n, ncclUint64, ncclMax, impl_->comm,
                              static_cast<hipStream_t>(stream)));
@@ -106,21 +113,31 @@ void RcclTransport::check_async() const {
     if (st != ncclSuccess) throw Error(std::string("RCCL async error: ") + ncclGetErrorString(st));
 }
 
-bool RcclTransport::wait_stream(void* stream) {
-    hipStream_t s = static_cast<hipStream_t>(stream);
+double watchdog_limit_s() {
     static const double limit = [] {
         const char* e = std::getenv("WAVE3D_WATCHDOG_S");
-        return e ? std::atof(e) : 600.0;
+        return e ? std::atof(e) : 120.0;
     }();
-    const auto t0 = std::chrono::steady_clock::now();
+    return limit;
+}
+
+bool RcclTransport::wait_stream(void* stream, const std::function<long()>* progress) {
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    const double limit = watchdog_limit_s();
+    auto t0 = std::chrono::steady_clock::now();
+    long seen = progress ? (*progress)() : 0;
     for (int spin = 0;; ++spin) {
         const hipError_t q = hipStreamQuery(s);
         if (q == hipSuccess) break;
         if (q != hipErrorNotReady) HIP_CHECK_T(q);
         ncclResult_t st = ncclSuccess;
         NCCL_CHECK(ncclCommGetAsyncError(impl_->comm, &st));
-        const double el =
-            std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        const auto now = std::chrono::steady_clock::now();
+        if (progress && (spin & 63) == 0) {
+            const long p = (*progress)();
+            if (p != seen) seen = p, t0 = now;  // the device moved on: restart the clock
+        }
+        const double el = std::chrono::duration<double>(now - t0).count();
         if (st != ncclSuccess || (limit > 0 && el > limit)) {
             (void)ncclCommAbort(impl_->comm);
             impl_->comm = nullptr;

@@ -26,6 +26,7 @@ public:
     int rank() const override { return rank_; }
     int size() const override { return size_; }
     bool device() const override { return true; }
+    int comm_size() const override;  // ncclCommCount
     void exchange(const std::vector<Message>& sends, const std::vector<Message>& recvs,
                   void* stream) override;
     void allreduce_max_u64(u64* data, size_t n, void* stream) override;
@@ -34,9 +35,10 @@ public:
     // Async-error watchdog: throws if the communicator reported an error.
     void check_async() const;
     // Polls the stream and the communicator's async error; aborts the communicator and throws
-    // after WAVE3D_WATCHDOG_S seconds (default 600) without progress, so a dead peer ends the
-    // run with an error instead of a hang.
-    bool wait_stream(void* stream) override;
+    // after WAVE3D_WATCHDOG_S seconds (default 120, below the benchmark driver's timeout)
+    // without progress — measured from the last growth of `progress` when given — so a dead
+    // peer ends the run with an error instead of a hang.
+    bool wait_stream(void* stream, const std::function<long()>* progress = nullptr) override;
 
 private:
     struct Impl;

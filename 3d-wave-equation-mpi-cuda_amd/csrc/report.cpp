@@ -92,7 +92,8 @@ std::string json_summary(const Config& c, const RunResult& r) {
       << ", \"dims\": [" << r.dims[0] << ", " << r.dims[1] << ", " << r.dims[2] << "]"
       << ", \"dtype\": \"" << dtype_name(r.dtype) << "\", \"backend\": \"" << r.backend
       << "\", \"kernel\": \"" << r.kernel << "\", \"transport\": \"" << r.transport << "\""
-      << ", \"overlap\": " << (c.overlap ? "true" : "false")
+      << ", \"overlap\": " << (r.overlap ? "true" : "false")
+      << ", \"comm_size\": " << r.comm_size
       << ", \"courant\": " << jnum(r.courant) << ", \"total_ms\": " << jnum(r.t.total_ms)
       << ", \"init_ms\": " << jnum(r.t.init_ms) << ", \"loop_ms\": " << jnum(r.t.loop_ms)
       << ", \"exchange_ms\": " << jnum(r.t.exchange_ms) << ", \"comm_ms\": " << jnum(r.t.comm_ms)

@@ -36,6 +36,8 @@ struct RunResult {
     std::string abort_reason;
     int resumed_from = -1;
     bool graph = false;  // time loop replayed as one hipGraph
+    bool overlap = false;  // interior/shell split with the halo on a second stream (effective)
+    int comm_size = 0;     // ranks the transport's communicator reports (ncclCommCount), 0 = none
 
     double points() const { return double(N + 1) * double(N + 1) * double(N + 1); }
     // Mpoints/s = (N+1)^3 * timesteps / t  (BASELINE.md metric definition)

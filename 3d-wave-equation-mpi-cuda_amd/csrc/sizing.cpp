@@ -31,8 +31,9 @@ static void parse_tb(const std::string& name, int& rows, int& waves, int& occ) {
 
 Layout plan_layout(const Config& c, int world) {
     Layout l;
-    // "auto": temporal blocking (tb2, measured fastest on MI355X, profiles/); across ranks
-    // x slabs unless --dims asks for another decomposition (then 2-deep y/z halos too)
+    // "auto": temporal blocking (tb2, measured fastest on MI355X, profiles/). The process
+    // grid is MPI_Dims_create's as in the reference (2x2x2 at 8 ranks; y/z splits get 2-deep
+    // row/column halos); `--dims P,1,1` selects x slabs (contiguous planes, 2 peers)
     const bool auto_tb = c.kernel == "auto";
     const bool tb3 = c.kernel.rfind("tb3", 0) == 0;
     l.tb = auto_tb || tb3 || c.kernel.rfind("tb2", 0) == 0;
@@ -44,11 +45,7 @@ Layout plan_layout(const Config& c, int world) {
     l.G = l.depth;      // ghost depth = layers per sweep
     l.L = l.depth + 2;  // 3 / 4 / 5 time levels (tb3: C never stored, D and E written)
     for (int a = 0; a < 3; ++a) l.dims[a] = c.dims[a];
-    // temporal blocking across ranks: 2-deep x halos, so the decomposition is x slabs
-    if (l.tb && world > 1 && !(c.dims[0] || c.dims[1] || c.dims[2])) {
-        l.dims[0] = world;
-        l.dims[1] = l.dims[2] = 1;
-    }
+    (void)world;
     return l;
 }
 

@@ -26,12 +26,38 @@ CONFIGS = {
     "gpu512": dict(problem=WaveProblem(512, timesteps=100), backend="hip", Np=1, dims=None),
     # N=512^3 fp64 on 2 MI355X, slab decomposition (2x1x1)
     "gpu512x2": dict(problem=WaveProblem(512, timesteps=100), backend="hip", Np=2, dims=[2, 1, 1]),
+    # config 4's grid on 4 MI355X (MPI_Dims_create(4) = 2x2x1; bench.py --gpus 4)
+    "gpu1024x4": dict(problem=WaveProblem(1024, timesteps=100), backend="hip", Np=4, dims=[2, 2, 1]),
     # N=1024^3 fp64 on 8 MI355X, 2x2x2 blocks (6-face deep halos, interior/shell overlap)
     "gpu1024x8": dict(problem=WaveProblem(1024, timesteps=100), backend="hip", Np=8, dims=[2, 2, 2]),
     # N=2048^3 fp32 on 8 MI355X
     "gpu2048x8_fp32": dict(problem=WaveProblem(2048, timesteps=200, dtype="fp32"), backend="hip", Np=8,
                            dims=None),
 }
+
+
+# bench.py --gpus n: the BASELINE.json config for that GPU count, each backed by a golden
+# L-inf (decomposition-invariant: the reference's errors are identical for every P).
+#   1: config 2 (N=512, one GPU)              2: config 3 (N=512, 2x1x1 slabs)
+#   4: config 4's grid on MPI_Dims_create(4)  8: config 4 (N=1024, 2x2x2 blocks)
+# 1 -> 8 is weak scaling (1025^3/8 ~= 513^3 nodes per GPU); 2 and 4 are strong-scaling points
+# of the 512^3 and 1024^3 grids.
+BENCH_BY_GPUS = {
+    1: dict(N=512, dims=None, scaling="weak", config="gpu512"),
+    2: dict(N=512, dims=[2, 1, 1], scaling="strong", config="gpu512x2"),
+    4: dict(N=1024, dims=[2, 2, 1], scaling="strong", config="gpu1024x4"),
+    8: dict(N=1024, dims=[2, 2, 2], scaling="weak", config="gpu1024x8"),
+}
+
+
+def bench_plan(n_gpus: int) -> dict:
+    """Global N, decomposition, scaling kind and golden of the benchmark at n_gpus."""
+    if n_gpus in BENCH_BY_GPUS:
+        p = dict(BENCH_BY_GPUS[n_gpus])
+    else:
+        p = dict(N=weak_scaling_N(n_gpus), dims=None, scaling="weak", config=f"weak{n_gpus}")
+    p["golden"] = GOLDEN_LINF.get((p["N"], 100))
+    return p
 
 
 def weak_scaling_N(n_gpus: int, base_N: int = 512) -> int:

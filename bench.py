@@ -7,12 +7,21 @@ N=512^3 fp64. One benchmark *step* is one complete solve exactly as timed by the
 layer, `timesteps` leapfrog layers, the fused per-layer max-error evaluation and the final
 cross-rank MAX reduction. Mpoints/s = (N+1)^3 * timesteps * steps / t_wall.
 
-Scaling is weak: per-GPU work is fixed at ~513^3 nodes, the global grid grows with the GPU
-count (1 GPU: N=512 = BASELINE config 2; 8 GPUs: N=1024 = BASELINE config 4's grid). The
-default kernel is temporal blocking (2 layers per sweep, 16 instead of 24 B/node/layer),
-which decomposes into x slabs with 2-deep RCCL halos; `--kernel march2` selects the
-single-step kernel on the MPI-style 3-D decomposition (2x2x2 at 8 GPUs, 6-face halos).
-Data: the analytic initial condition on a synthetic grid (the reference's own test problem).
+`--gpus n` runs the BASELINE.json config for that GPU count, each with a golden L-inf from
+the reference (the reference's errors are identical for every P):
+
+    1 GPU : N=512,  1x1x1          (config 2)      golden 6.03381e-07
+    2 GPUs: N=512,  2x1x1 slabs    (config 3)      golden 6.03381e-07   strong vs 1 GPU
+    4 GPUs: N=1024, 2x2x1          (config 4 grid) golden 8.04265e-08   strong vs 8 GPUs
+    8 GPUs: N=1024, 2x2x2 blocks   (config 4)      golden 8.04265e-08   weak vs 1 GPU
+
+The decomposition is MPI_Dims_create's, as in the reference (mpi_new.cpp:409-433); `--dims`
+overrides it. The default kernel is temporal blocking (2 layers per sweep, 16 instead of
+24 B/node/layer) with 2-deep RCCL halos; `--kernel march2` selects the single-step kernel.
+The JSON line states what ran: N and dtype in the metric, dims, the effective overlap,
+the transport and the ranks RCCL itself reports (ncclCommCount), and whether the L-inf
+matches the golden. Data: the analytic initial condition on a synthetic grid (the
+reference's own test problem).
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
@@ -27,7 +36,7 @@ import time
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
-METRIC = "Mpoints/sec (whole node) + L∞ error vs analytic, N=512³ fp64"
+METRIC = "Mpoints/sec (whole node) + L∞ error vs analytic, N={N}³ {dtype}"  # BASELINE.json at N=512
 
 
 def main() -> int:
@@ -35,7 +44,8 @@ def main() -> int:
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5, help="timed solves")
     ap.add_argument("--warmup", type=int, default=2, help="untimed solves")
-    ap.add_argument("--N", type=int, default=0, help="override global N (default: weak scaling from 512)")
+    ap.add_argument("--N", type=int, default=0, help="override global N (default: the BASELINE config)")
+    ap.add_argument("--dims", default="", help="process grid a,b,c (default: the BASELINE config's)")
     ap.add_argument("--timesteps", type=int, default=100,
                     help="layers per solve (0: smallest stable count with margin, C <= 0.5)")
     ap.add_argument("--fill-hbm", type=float, default=0.0,
@@ -81,7 +91,9 @@ def main() -> int:
     elif a.backend == "hip":
         torch.cuda.set_device(0)
 
-    N = a.N or presets.weak_scaling_N(n_gpus)
+    plan = presets.bench_plan(n_gpus)
+    N = a.N or plan["N"]
+    dims = [int(x) for x in a.dims.split(",")] if a.dims else (None if a.N else plan["dims"])
     if a.fill_hbm > 0:
         if a.backend != "hip":
             print("bench: --fill-hbm needs the hip backend", file=sys.stderr)
@@ -98,7 +110,7 @@ def main() -> int:
     prob = wave3d.WaveProblem(N, timesteps=a.timesteps, dtype=a.dtype)
     if not prob.stable():
         print(f"bench: warning: C={prob.courant:.3f} > 1/sqrt(3) (unstable)", file=sys.stderr)
-    solver = wave3d.WaveSolver(prob, a.backend, transport=transport, Np=n_gpus, kernel=a.kernel,
+    solver = wave3d.WaveSolver(prob, a.backend, transport=transport, Np=n_gpus, kernel=a.kernel, dims=dims,
                                chunk=a.chunk, overlap=not a.no_overlap, profile=a.profile,
                                device=(torch.cuda.current_device() if a.backend == "hip" else None))
     args = solver.args()
@@ -128,9 +140,10 @@ def main() -> int:
     pts = (N + 1) ** 3
     value = pts * a.timesteps * a.steps / elapsed / 1e6
     base = presets.BASELINE_MPTS.get(N, presets.BASELINE_MPTS[512])
+    golden = presets.GOLDEN_LINF.get((N, a.timesteps)) if a.dtype == "fp64" else None
     dims = res["dims"]
     out = {
-        "metric": METRIC,
+        "metric": METRIC.format(N=N, dtype=a.dtype),
         "value": round(value, 3),
         "unit": "Mpoints/s",
         "n_gpus": n_gpus,
@@ -138,7 +151,7 @@ def main() -> int:
         "warmup": a.warmup,
         "ms_per_step": round(elapsed / a.steps * 1e3, 4),
         "higher_is_better": True,
-        "scaling": "strong" if a.N else "weak",  # --N fixes the global grid
+        "scaling": "strong" if a.N else plan["scaling"],  # --N fixes the global grid
         "vs_baseline": round(value / base, 3),
         "dtype": a.dtype,
         "data": "synthetic (analytic initial condition u=sin(2pi x/Lx)sin(pi y/Ly)sin(pi z/Lz))",
@@ -148,23 +161,30 @@ def main() -> int:
             "seq_len": N + 1,
             "parallelism": f"dd{dims[0]}x{dims[1]}x{dims[2]}-{res['kernel']}"
                            + ("" if n_gpus == 1 else f"-{res['transport']}"),
+            "baseline_config": None if a.N else plan["config"],
             "N": N,
             "timesteps": a.timesteps,
+            "dims": dims,
             "kernel": res["kernel"],
-            "overlap": not a.no_overlap,
+            "overlap": bool(res["overlap"]),  # effective (off when there is no remote halo)
+            "transport": res["transport"],
             "hip_graph": bool(res.get("graph", False)),
             "fill_hbm": a.fill_hbm or None,
             "device_bytes_per_gpu": C.memory_plan(args, n_gpus)["bytes_per_rank"]
                                      if a.backend == "hip" else None,
         },
+        # ranks the halo communicator spans as RCCL reports them (ncclCommCount), None without one
+        "rccl_nranks": res["comm_size"] if res["transport"] == "rccl" else None,
         "linf_abs": res["linf_abs"],
         "linf_final_layer": res["timesteps"],
+        "linf_golden": golden,
+        "linf_ok": None if golden is None else f"{res['linf_abs']:.6g}" == f"{golden:.6g}",
         "courant": round(prob.courant, 4),
         "solver_ms_per_step": round(sum(res["solve_ms"]) / max(1, len(res["solve_ms"])), 4),
+        # the reference's timer breakdown of the last solve, max over ranks (mpi_new.cpp:368-371)
+        "timers_ms": {k: round(res[k], 4) for k in ("loop_ms", "exchange_ms", "error_ms", "total_ms")},
         "baseline_mpts": base,
     }
-    if a.profile:
-        out["profile_ms"] = {k: res[k] for k in ("loop_ms", "exchange_ms", "error_ms", "total_ms")}
     if rank == 0:
         print(json.dumps(out), flush=True)
     # explicit teardown while HIP and the process group are alive: the session (which keeps the

@@ -39,7 +39,10 @@ def _check(r, n, steps, warmup):
     with open(os.path.join(ROOT, "BASELINE.json")) as f:
         metric = json.load(f)["metric"]
     assert FIELDS <= set(r)
-    assert r["metric"] == metric and r["unit"] == "Mpoints/s" and r["higher_is_better"] is True
+    N = r["config"]["N"]
+    # BASELINE.json's metric, stating the N that actually ran (identical at N=512 fp64)
+    assert r["metric"] == metric.replace("N=512³", f"N={N}³") and r["unit"] == "Mpoints/s"
+    assert r["higher_is_better"] is True
     assert r["n_gpus"] == n and r["steps"] == steps and r["warmup"] == warmup
     assert r["value"] > 0 and r["ms_per_step"] > 0 and r["dtype"] == "fp64"
     cfg = r["config"]
@@ -68,3 +71,19 @@ def test_bench_gpu_default_config_short():
     _check(r, 1, 1, 1)
     assert r["scaling"] == "weak" and r["config"]["N"] == 512 and r["config"]["timesteps"] == 100
     assert f"{r['linf_abs']:.6g}" == "6.03381e-07"  # golden N=512 K=100
+    assert r["linf_golden"] == 6.03381e-07 and r["linf_ok"] is True
+    assert r["config"]["dims"] == [1, 1, 1] and r["config"]["overlap"] is False  # no remote halo
+    assert r["config"]["baseline_config"] == "gpu512" and r["rccl_nranks"] is None
+
+
+def test_bench_plan_maps_gpu_counts_to_baseline_configs(C):
+    from wave3d.models import presets
+
+    assert presets.bench_plan(1) == dict(N=512, dims=None, scaling="weak", config="gpu512",
+                                         golden=6.03381e-07)
+    p2, p4, p8 = presets.bench_plan(2), presets.bench_plan(4), presets.bench_plan(8)
+    assert (p2["N"], p2["dims"], p2["golden"]) == (512, [2, 1, 1], 6.03381e-07)
+    assert (p4["N"], p4["dims"], p4["golden"]) == (1024, [2, 2, 1], 8.04265e-08)
+    assert (p8["N"], p8["dims"], p8["golden"]) == (1024, [2, 2, 2], 8.04265e-08)
+    assert p8["scaling"] == "weak" and p2["scaling"] == "strong"
+    assert C.dims_create(4, [0, 0, 0]) == p4["dims"] and C.dims_create(8, [0, 0, 0]) == p8["dims"]

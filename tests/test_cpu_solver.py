@@ -1,5 +1,7 @@
 """OpenMP oracle: goldens (Appendix C), decomposition invariance, bitwise agreement with the
 plain-PyTorch solve, fp32, checkpoint/resume, fault detection."""
+import os
+
 import pytest
 
 
@@ -89,6 +91,43 @@ def test_checkpoint_resume_bitwise(C, tmp_path):
     # a different configuration is refused
     with pytest.raises(Exception):
         _solve(wave3d.WaveProblem(20, timesteps=15), ranks=4, resume=str(tmp_path))
+
+
+def test_checkpoint_generations_and_agreed_resume(C, tmp_path):
+    """Two complete generations per rank are kept; a rank whose newest file is missing (a crash
+    while writing it) makes every rank resume from the newest layer they all have."""
+    import wave3d
+
+    p = wave3d.WaveProblem(20, timesteps=14, ic="shifted")
+    full = _solve(p, ranks=3)
+    d = str(tmp_path)
+    _solve(p, ranks=3, checkpoint_every=3, checkpoint_dir=d)
+    for r in range(3):
+        assert C.checkpoint_layers(d, r) == [9, 12]
+    os.remove(os.path.join(d, "ckpt_r1_L12.bin"))  # rank 1 died writing layer 12
+    res = _solve(p, ranks=3, resume=d)
+    assert res.extra["resumed_from"] == 9
+    assert res.max_abs == full.max_abs and res.max_rel == full.max_rel
+    os.remove(os.path.join(d, "ckpt_r2_L9.bin"))  # no layer common to every rank any more
+    with pytest.raises(Exception, match="common"):
+        _solve(p, ranks=3, resume=d)
+
+
+def test_checkpoint_agreed_resume_multiprocess(C, tmp_path):
+    """The same agreement across processes (gloo host transport, 2 ranks): rank 1's newest
+    checkpoint is missing, both processes resume from layer 9 and reproduce the full run."""
+    from test_dist import torchrun
+
+    args = ["20", "1", "pi", "pi", "pi", "1", "14", "--ic", "shifted", "--threads", "1"]
+    d = str(tmp_path)
+    full = torchrun(2, ["--backend", "cpu", "--transport", "gloo"], args)
+    torchrun(2, ["--backend", "cpu", "--transport", "gloo"],
+             args + ["--checkpoint-every", "3", "--checkpoint-dir", d])
+    assert C.checkpoint_layers(d, 0) == [9, 12] and C.checkpoint_layers(d, 1) == [9, 12]
+    os.remove(os.path.join(d, "ckpt_r1_L12.bin"))
+    res = torchrun(2, ["--backend", "cpu", "--transport", "gloo"], args + ["--resume", d])
+    assert res["resumed_from"] == 9
+    assert res["max_abs"] == full["max_abs"] and res["max_rel"] == full["max_rel"]
 
 
 def test_fault_injection_detected(C):

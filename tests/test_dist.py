@@ -65,7 +65,7 @@ def test_hip_multiprocess_shared_gpu(C, single_cpu, P, overlap):
 @pytest.mark.parametrize("P,kernel", [(2, "tb2r4"), (4, "tb2")])
 def test_hip_multiprocess_temporal_blocking(C, single_cpu, P, kernel):
     r = torchrun(P, ["--backend", "hip", "--transport", "staged", "--shared-device"],
-                 ARGS + ["--kernel", kernel])
+                 ARGS + ["--kernel", kernel, "--dims", f"{P},1,1"])
     assert r["dims"] == [P, 1, 1] and r["kernel"] == kernel
     assert r["max_abs"] == single_cpu["max_abs"] and r["max_rel"] == single_cpu["max_rel"]
 
@@ -84,5 +84,22 @@ def test_hip_multiprocess_temporal_blocking_3d(C, single_cpu, P, dims):
 @pytest.mark.gpu
 def test_rccl_transport_single_rank(C, single_cpu):
     r = torchrun(1, ["--backend", "hip", "--transport", "rccl"], ARGS)
-    assert r["transport"] == "rccl"
+    assert r["transport"] == "rccl" and r["comm_size"] == 1
     assert r["max_abs"] == single_cpu["max_abs"] and r["max_rel"] == single_cpu["max_rel"]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kernel,overlap", [("march2", True), ("march2", False), ("tb2", True),
+                                            ("tb2", False), ("tb3", True)])
+def test_rccl_self_send(C, single_cpu, kernel, overlap):
+    """--x-self-transport: the periodic x wrap of the one x rank travels as ncclSend/ncclRecv
+    to itself (x planes, the deep temporal-blocking planes) instead of the fused local wrap,
+    so the RCCL point-to-point path of the multi-GPU halo runs on a one-GPU lease; the
+    per-layer errors must equal the OpenMP oracle's bit for bit."""
+    extra = ["--kernel", kernel, "--x-self-transport"] + ([] if overlap else ["--no-overlap"])
+    r = torchrun(1, ["--backend", "hip", "--transport", "rccl"], ARGS + extra)
+    assert r["transport"] == "rccl" and r["comm_size"] == 1 and r["kernel"] == kernel
+    assert r["overlap"] == overlap
+    assert r["exchange_ms"] > 0  # halo messages were timed on the stream
+    assert r["max_abs"] == single_cpu["max_abs"] and r["max_rel"] == single_cpu["max_rel"]
+

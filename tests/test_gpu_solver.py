@@ -34,18 +34,15 @@ def test_golden_n32(C, kernel):
 @pytest.mark.parametrize("kernel", ["auto", "march2", "naive"])
 @pytest.mark.parametrize("ranks,overlap", [(2, True), (2, False), (4, True), (8, True), (8, False), (3, True)])
 def test_decomposition_invariance(C, ranks, overlap, kernel):
-    """auto = temporal blocking on x slabs; march2/naive = single-step on the MPI-style 3-D
-    decomposition (2x2x2 at 8 ranks) with 6-face halos."""
+    """auto = temporal blocking (2-deep halos), march2/naive = single-step (6-face halos), all
+    on the MPI_Dims_create decomposition (2x2x2 at 8 ranks) as in the reference."""
     import wave3d
 
     p = wave3d.WaveProblem(40, Lx=1.3, Ly="pi", Lz=2.0, timesteps=15, ic="shifted")
     base = _solve(p, kernel="march2")
     r = _solve(p, ranks=ranks, overlap=overlap, kernel=kernel)
     assert r.transport == "loopback"
-    if kernel == "auto":
-        assert r.dims == [ranks, 1, 1]
-    elif ranks == 8:
-        assert r.dims == [2, 2, 2]
+    assert r.dims == C.dims_create(ranks, [0, 0, 0])
     assert r.max_abs == base.max_abs and r.max_rel == base.max_rel
 
 
@@ -97,7 +94,7 @@ def test_checkpoint_resume(C, tmp_path, kernel, K):
     full = _solve(p, ranks=2, kernel=kernel)
     d = str(tmp_path)
     _solve(p, ranks=2, checkpoint_every=5, checkpoint_dir=d, kernel=kernel)
-    assert os.path.exists(os.path.join(d, "ckpt_r0.bin"))
+    assert os.path.exists(os.path.join(d, "ckpt_r0_L10.bin"))
     res = _solve(p, ranks=2, resume=d, kernel=kernel)
     assert res.extra["resumed_from"] == 10
     assert res.max_abs == full.max_abs and res.max_rel == full.max_rel
@@ -182,7 +179,7 @@ def test_temporal_blocking_slabs_loopback(C, ranks, overlap, kernel):
     for K in (9, 10):
         p = wave3d.WaveProblem(45, Lx=1.3, Ly="pi", Lz=2.0, timesteps=K, ic="shifted")
         base = _solve(p, backend="cpu", threads=4)
-        r = _solve(p, ranks=ranks, overlap=overlap, kernel=kernel)
+        r = _solve(p, ranks=ranks, overlap=overlap, kernel=kernel, dims=[ranks, 1, 1])
         assert r.dims == [ranks, 1, 1] and r.kernel == kernel
         assert r.max_abs == base.max_abs and r.max_rel == base.max_rel
 

@@ -8,11 +8,13 @@ import pytest
 ARGS = ["512", "1", "pi", "pi", "pi", "1", "100"]
 
 
-def test_layout_auto_is_temporal_blocking_on_slabs(C):
+def test_layout_auto_is_temporal_blocking_on_dims_create(C):
     p1 = C.memory_plan(ARGS, 1)
     assert p1["tb"] and p1["ghost"] == 2 and p1["levels"] == 4
-    p8 = C.memory_plan(ARGS, 8)
-    assert p8["tb"] and p8["dims"] == [8, 1, 1]
+    p8 = C.memory_plan(ARGS, 8)  # no override: MPI_Dims_create's 2x2x2, as the reference
+    assert p8["tb"] and p8["dims"] == [0, 0, 0]
+    s8 = C.memory_plan(ARGS + ["--dims", "8,1,1"], 8)  # x slabs on request
+    assert s8["tb"] and s8["dims"] == [8, 1, 1]
     m = C.memory_plan(ARGS + ["--kernel", "march2"], 8)
     assert not m["tb"] and m["ghost"] == 1 and m["levels"] == 3 and m["dims"] == [0, 0, 0]
     y = C.memory_plan(ARGS + ["--dims", "2,2,2"], 8)  # temporal blocking with y/z halos

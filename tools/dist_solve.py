@@ -43,7 +43,8 @@ def main():
     r = C.run(args, a.backend, tr, False, rank == 0)
     if rank == 0:
         keep = ("N", "timesteps", "nprocs", "dims", "transport", "kernel", "max_abs", "max_rel",
-                "total_ms", "aborted", "abort_layer", "resumed_from")
+                "total_ms", "loop_ms", "exchange_ms", "comm_ms", "overlap", "comm_size",
+                "aborted", "abort_layer", "resumed_from")
         print("RESULT " + json.dumps({k: r[k] for k in keep}), flush=True)
     dist.barrier()
     del tr
