@@ -61,24 +61,37 @@ struct RelArg {
     __device__ __forceinline__ void add(T ea, T fa) {
 #pragma clang fp contract(off)
         const T p1 = ea * den, p2 = num * fa;
-        const T e1 = fma_t(ea, den, -p1), e2 = fma_t(num, fa, -p2);
-        if (p1 > p2 || (p1 == p2 && e1 > e2)) num = ea, den = fa;
+        bool up = p1 > p2;
+        // exact tie-break on the FMA residuals only where the rounded products tie (rare:
+        // mirror-symmetric nodes); the wave skips the block when no lane ties
+        if (__builtin_expect(p1 == p2, 0)) up = fma_t(ea, den, -p1) > fma_t(num, fa, -p2);
+        if (up) num = ea, den = fa;
     }
     __device__ __forceinline__ T value() const { return num / den; }
 };
 
+__device__ __forceinline__ double fmax_t(double a, double b) { return __builtin_fmax(a, b); }
+__device__ __forceinline__ float fmax_t(float a, float b) { return __builtin_fmaxf(a, b); }
+
+// Per node: |u - f| into the running maximum and the relative-error argmax, and u into `chk`.
+// The maximum is v_max (IEEE maxNum): a NaN error is ignored exactly like the reference's
+// `if (e > m) m = e` (mpi_new.cpp:343-344; errors are arithmetic results, never signalling
+// NaNs). `chk` is the sum of the layer's values: non-finite iff some value was NaN/Inf (or
+// the values overflow a double, i.e. the run diverged anyway) — one add per node instead of
+// a compare-and-or; commit_errors() turns it into the nonfinite flag.
 template <class T>
 __device__ __forceinline__ void accumulate_error_dev(T u, T f, T& mabs, RelArg<T>& mrel) {
 #pragma clang fp contract(off)
     const T ea = absval(u - f);
-    if (ea > mabs) mabs = ea;
+    mabs = fmax_t(mabs, ea);
     mrel.add(ea, absval(f));
 }
 
 // Workgroup reduction of the running maxima + one atomic per slot (race-free, no
 // divergent barrier: every thread reaches the __syncthreads, cf. Appendix B5).
 template <class T, int NW = kWaves>
-__device__ __forceinline__ void commit_errors(T ma, T mr, bool bad, u64* err) {
+__device__ __forceinline__ void commit_errors(T ma, T mr, T chk, u64* err) {
+    const bool bad = nonfinite(chk);
     __shared__ double red[2][NW];
     __shared__ int redb[NW];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;

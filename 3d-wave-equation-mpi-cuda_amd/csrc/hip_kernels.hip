@@ -182,7 +182,7 @@ __global__ void __launch_bounds__(kThreads) k_march(const StepParams<T> p) {
 
     T ma = T(kErrInit);
     RelArg<T> mr;
-    bool bad = false;
+    T chk = T(0);  // sum of the values (commit_errors: nonfinite flag)
 
     auto plane = [&](auto phase, const int i) {
         constexpr int P = decltype(phase)::value;
@@ -269,7 +269,7 @@ __global__ void __launch_bounds__(kThreads) k_march(const StepParams<T> p) {
                 if (k == p.zk1) p.zbuf1[i64(i - 1) * p.zrow + j] = x;
                 if (j == p.yj0) p.ybuf0[i64(i - 1) * p.yrow + k] = x;
                 if (j == p.yj1) p.ybuf1[i64(i - 1) * p.yrow + k] = x;
-                bad |= nonfinite(x);
+                chk += x;
                 if (erow) {
                     if constexpr (FAST) accumulate_error_dev(x, vget<L>(f, e), ma, mr);
                     else accumulate_error_dev(x, vget<L>(f, e), ma, mr);
@@ -288,7 +288,7 @@ __global__ void __launch_bounds__(kThreads) k_march(const StepParams<T> p) {
         plane(Ph<3>{}, i);
         if (++i > ie) break;
     }
-    commit_errors(ma, mr.value(), bad, p.err);
+    commit_errors(ma, mr.value(), chk, p.err);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -310,7 +310,7 @@ __global__ void __launch_bounds__(kThreads) k_naive(const StepParams<T> p) {
     const int j = B.j0 + tj * kNaiveTJ + w;
     T ma = T(kErrInit);
     RelArg<T> mr;
-    bool bad = false;
+    T chk = T(0);  // sum of the values (commit_errors: nonfinite flag)
     if (k >= B.k0 && k <= B.k1 && j <= B.j1) {
         const i64 si = p.si;
         const int rowoff = j * p.sj + k;
@@ -323,12 +323,12 @@ __global__ void __launch_bounds__(kThreads) k_naive(const StepParams<T> p) {
                                       p.hz2, p.yx2, p.yy2, p.yz2);
             const T v = FIRST ? taylor_first(c, lap, p.coef) : leapfrog(c, p.u2[o], lap, p.coef);
             store_point(p, i, j, k, o, rowoff, v);
-            bad |= nonfinite(v);
+            chk += v;
             if (i >= p.ei0 && i <= p.ei1)
                 accumulate_error_dev(v, analytic(p.tx[i], tyj, tzk, p.ct), ma, mr);
         }
     }
-    commit_errors(ma, mr.value(), bad, p.err);
+    commit_errors(ma, mr.value(), chk, p.err);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -345,7 +345,7 @@ __global__ void __launch_bounds__(kThreads) k_flat(const StepParams<T> p) {
     const i64 e = i64(bid - B.block_begin) * kThreads + threadIdx.x;
     T ma = T(kErrInit);
     RelArg<T> mr;
-    bool bad = false;
+    T chk = T(0);  // sum of the values (commit_errors: nonfinite flag)
     if (e < total) {
         const int k = B.k0 + int(e % nk);
         const i64 r = e / nk;
@@ -360,10 +360,10 @@ __global__ void __launch_bounds__(kThreads) k_flat(const StepParams<T> p) {
                                   p.yz2);
         const T v = FIRST ? taylor_first(c, lap, p.coef) : leapfrog(c, p.u2[o], lap, p.coef);
         store_point(p, i, j, k, o, rowoff, v);
-        bad |= nonfinite(v);
+        chk += v;
         if (i >= p.ei0 && i <= p.ei1) accumulate_error_dev(v, analytic(p.tx[i], p.ty[j], p.tz[k], p.ct), ma, mr);
     }
-    commit_errors(ma, mr.value(), bad, p.err);
+    commit_errors(ma, mr.value(), chk, p.err);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -378,7 +378,7 @@ __global__ void __launch_bounds__(kThreads) k_init(T* u, i64 si, int sj, Box bx,
     const int ie = min(bx.i1, ib + chunk - 1);
     T ma = T(kErrInit);
     RelArg<T> mr;
-    bool bad = false;
+    T chk = T(0);  // sum of the values (commit_errors: nonfinite flag)
     if (k <= bx.k1 && j <= bx.j1) {
         const int rowoff = j * sj + k;
         const T tyj = ty[j], tzk = tz[k];
@@ -388,11 +388,11 @@ __global__ void __launch_bounds__(kThreads) k_init(T* u, i64 si, int sj, Box bx,
 #pragma unroll
             for (int q = 0; q < kMaxWrap; ++q)
                 if (i == wrap.src[q]) u[i64(wrap.dst[q]) * si + rowoff] = f;
-            bad |= nonfinite(f);
+            chk += f;
             accumulate_error_dev(f, analytic(tx[i], tyj, tzk, ct), ma, mr);
         }
     }
-    commit_errors(ma, mr.value(), bad, err);
+    commit_errors(ma, mr.value(), chk, err);
 }
 
 template <class T>
