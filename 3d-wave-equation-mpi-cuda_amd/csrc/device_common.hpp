@@ -23,7 +23,7 @@ namespace {
 
 constexpr int kThreads = 256;
 constexpr int kWaves = kThreads / 64;
-constexpr int kTK = 64;                  // tile columns (k) = one wave64
+constexpr int kTK = kTileK;              // tile columns (k) = one wave64
 constexpr int kLW = kTK + 2;             // LDS row incl. k halos
 constexpr int kNaiveTJ = kWaves;         // naive kernel: one row per wave
 

@@ -27,6 +27,8 @@ struct GridView {
 
 // Up to this many boxes per launch (interior + 6 shell slabs).
 constexpr int kMaxBoxes = 7;
+constexpr int kTileK = 64;  // k columns per tile of the marching kernels (one wave64), tiles
+                            // start at k = 1 + 64 t
 
 struct StepCoefs {
     double hx2 = 1, hy2 = 1, hz2 = 1;  // h*h divisors

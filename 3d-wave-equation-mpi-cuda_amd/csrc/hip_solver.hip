@@ -248,6 +248,7 @@ private:
         HIP_CHECK(hipEventCreateWithFlags(&ev_end_, hipEventDefault));
         HIP_CHECK(hipEventCreateWithFlags(&ev_layer_, hipEventDisableTiming));
         HIP_CHECK(hipEventCreateWithFlags(&ev_halo_, hipEventDisableTiming));
+        HIP_CHECK(hipEventCreateWithFlags(&ev_shell_, hipEventDisableTiming));
         ranks_.resize(local_.size());
         const bool have_dims = cfg_.dims[0] || cfg_.dims[1] || cfg_.dims[2];
         for (size_t q = 0; q < local_.size(); ++q) {
@@ -392,7 +393,7 @@ private:
         ranks_.clear();
         if (s_comp_) (void)hipStreamDestroy(s_comp_);
         if (s_comm_) (void)hipStreamDestroy(s_comm_);
-        for (auto e : {ev_start_, ev_end_, ev_layer_, ev_halo_})
+        for (auto e : {ev_start_, ev_end_, ev_layer_, ev_halo_, ev_shell_})
             if (e) (void)hipEventDestroy(e);
         if (ts_host_) (void)hipHostFree(ts_host_);
         ts_host_ = ts_dev_ = nullptr;
@@ -548,13 +549,26 @@ private:
                 if (up >= 0) add(V, up, base + 3, 2, abox(n + 1, n + dA));
             }
         }
-        // the last layer within dA nodes of a received ghost depends on it (through the rings)
+        // the last layer within dA nodes of a received ghost depends on it (through the rings).
+        // The j/k shells are widened to whole tiles — TJ rows from the compute box's edge, k on
+        // the global 64-column tile grid — so the shell launch runs no partially filled tiles
+        // (a 2-column z shell used 2 of 64 lanes per tile and cost ~20 % of a sweep); the
+        // interior shrinks by the same nodes, so the total work is that of one full sweep. x
+        // shells stay dA planes thin: the march along i handles thin boxes at a small prologue.
+        // The shells also contain every plane / row / column the next exchange sends (the first
+        // and last x-ranks send one plane deeper, skipping the periodic duplicate plane), so the
+        // exchange can start as soon as the shells are done, while the interior still runs.
         Box c = R.compute, in = c;
-        if (!R.plan.self_x) in.i0 = std::max(in.i0, 1 + dA), in.i1 = std::min(in.i1, X - dA);
-        if (t.nbr[1][0] >= 0) in.j0 = std::max(in.j0, 1 + dA);
-        if (t.nbr[1][1] >= 0) in.j1 = std::min(in.j1, Y - dA);
-        if (t.nbr[2][0] >= 0) in.k0 = std::max(in.k0, 1 + dA);
-        if (t.nbr[2][1] >= 0) in.k1 = std::min(in.k1, Z - dA);
+        const int TJ = tb_rows_ * tb_waves_;
+        if (!R.plan.self_x) {
+            const int xs = t.dims[0] > 1 ? 1 : 0;  // one x rank messaging itself: both ends
+            in.i0 = std::max(in.i0, 1 + dA + ((t.first(0) || !xs) ? 1 : 0));
+            in.i1 = std::min(in.i1, X - dA - ((t.last(0) || !xs) ? 1 : 0));
+        }
+        if (t.nbr[1][0] >= 0) in.j0 = std::max(in.j0, std::max(1 + dA, c.j0 + TJ));
+        if (t.nbr[1][1] >= 0) in.j1 = std::min(in.j1, std::min(Y - dA, c.j1 - TJ));
+        if (t.nbr[2][0] >= 0) in.k0 = std::max(in.k0, 1 + kTileK * ((dA + kTileK - 1) / kTileK));
+        if (t.nbr[2][1] >= 0) in.k1 = std::min(in.k1, kTileK * ((Z - dA) / kTileK));
         R.tb_interior = in;
         auto add = [&](Box b) {
             if (!b.empty()) R.tb_shell.push_back(b);
@@ -928,6 +942,7 @@ private:
             // temporal blocking: 3 (tb3) or 2 layers per sweep; shorter tails use the
             // two-layer sweep / a single step (the storage has ghosts for the deepest)
             const int span = (tbd_ == 3 && n + 2 <= K) ? 3 : ((tb_ && n + 1 <= K) ? 2 : 1);
+            bool comm_follows = false;  // the comm stream already runs behind this layer's shells
             for (int q = n; q < n + span; ++q) guard_checkpoint_level(lvl(q), s_comp_);
             if (cfg_.print_layers && !cfg_.quiet && ranks_[0].topo.rank == 0)
                 for (int q = n; q < n + span; ++q) std::cout << "calculating layer " << q << "\n";
@@ -956,12 +971,23 @@ private:
                     sweep3(R, n, s_comp_);
                 }
             } else if (span == 2 && overlap_) {
-                for (auto& R : ranks_)
-                    if (!R.tb_interior.empty()) sweep(R, n, s_comp_, &R.tb_interior, 1);
-                HIP_CHECK(hipStreamWaitEvent(s_comp_, ev_halo_, 0));
+                // Shells on the (high-priority) comm stream right behind the previous halo,
+                // concurrently with the interior on the compute stream: both read only levels
+                // of earlier sweeps and write disjoint nodes. The shells need the interior of
+                // the previous sweep (their rings reach into it); the compute stream waits for
+                // the shells before the next interior (whose rings reach into them). The next
+                // exchange follows the shells on the comm stream without waiting for the
+                // interior — the shells contain every node it sends.
+                HIP_CHECK(hipEventRecord(ev_layer_, s_comp_));
+                HIP_CHECK(hipStreamWaitEvent(s_comm_, ev_layer_, 0));
                 for (auto& R : ranks_)
                     if (!R.tb_shell.empty())
-                        sweep(R, n, s_comp_, R.tb_shell.data(), int(R.tb_shell.size()));
+                        sweep(R, n, s_comm_, R.tb_shell.data(), int(R.tb_shell.size()));
+                HIP_CHECK(hipEventRecord(ev_shell_, s_comm_));
+                for (auto& R : ranks_)
+                    if (!R.tb_interior.empty()) sweep(R, n, s_comp_, &R.tb_interior, 1);
+                HIP_CHECK(hipStreamWaitEvent(s_comp_, ev_shell_, 0));
+                comm_follows = true;
             } else if (span == 2) {
                 for (auto& R : ranks_) sweep(R, n, s_comp_);
             } else if (overlap_) {
@@ -980,7 +1006,7 @@ private:
                     if (!(span == 3 && q == n)) inject_after_compute(R, q, s_comp_, q == n + 1 && span == 3 ? n : q);
             mark(s_comp_, 1);
             const int last = n + span - 1;
-            if (last < K) issue_exchange(last);
+            if (last < K) issue_exchange(last, comm_follows);
             done = last;
             bool ck = false, stop = false;
             for (int q = n; q <= last; ++q) {
@@ -1046,10 +1072,12 @@ private:
         else exchange(n, s);
     }
 
-    void issue_exchange(int n) {
+    void issue_exchange(int n, bool comm_follows = false) {
         if (overlap_) {
-            HIP_CHECK(hipEventRecord(ev_layer_, s_comp_));
-            HIP_CHECK(hipStreamWaitEvent(s_comm_, ev_layer_, 0));
+            if (!comm_follows) {
+                HIP_CHECK(hipEventRecord(ev_layer_, s_comp_));
+                HIP_CHECK(hipStreamWaitEvent(s_comm_, ev_layer_, 0));
+            }
             mark(s_comm_, 2);
             any_exchange(n, s_comm_);
             mark(s_comm_, 3);
@@ -1291,6 +1319,7 @@ private:
     std::vector<double> ckpt_abs_, ckpt_rel_;
     hipStream_t s_comp_ = nullptr, s_comm_ = nullptr;
     hipEvent_t ev_start_ = nullptr, ev_end_ = nullptr, ev_layer_ = nullptr, ev_halo_ = nullptr;
+    hipEvent_t ev_shell_ = nullptr;  // shells of the current sweep done (comm stream)
     u64* ts_host_ = nullptr;       // timer-mark stamps (pinned, coherent host memory)
     u64* ts_dev_ = nullptr;        // its device address
     size_t ts_cap_ = 0;

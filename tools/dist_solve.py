@@ -44,6 +44,7 @@ def main():
     if rank == 0:
         keep = ("N", "timesteps", "nprocs", "dims", "transport", "kernel", "max_abs", "max_rel",
                 "total_ms", "loop_ms", "exchange_ms", "comm_ms", "overlap", "comm_size",
+                "solve_ms", "mpts_per_s_best",
                 "aborted", "abort_layer", "resumed_from")
         print("RESULT " + json.dumps({k: r[k] for k in keep}), flush=True)
     dist.barrier()
