@@ -39,8 +39,11 @@ Layout plan_layout(const Config& c, int world) {
     l.tb = auto_tb || tb3 || c.kernel.rfind("tb2", 0) == 0;
     l.depth = tb3 ? 3 : (l.tb ? 2 : 1);
     if (tb3) l.rows = 2, l.waves = 8;  // measured best three-layer tile (profiles/)
-    // fp32: 16-row tiles (tb2r4, 95 VGPRs) beat 8-row ones by ~4 % at N=512
+    // fp32: 16-row tiles (tb2r4, 95 VGPRs) beat 8-row ones by ~4 % at N=512; fp64: 16-row
+    // tiles of 8 waves (tb2r2w8, 128 VGPRs, 2 workgroups per CU) beat 8-row ones by 2-3 %
+    // (profiles/sweep_tb2_vgpr128_r2.txt, profiles/ab_tiles_r2.txt)
     if (auto_tb && c.dtype == DType::F32) l.rows = 4;
+    if (auto_tb && c.dtype == DType::F64) l.waves = 8;
     if (l.tb && !auto_tb) parse_tb(c.kernel, l.rows, l.waves, l.occ);
     l.G = l.depth;      // ghost depth = layers per sweep
     l.L = l.depth + 2;  // 3 / 4 / 5 time levels (tb3: C never stored, D and E written)

@@ -77,7 +77,7 @@ def test_hip_multiprocess_temporal_blocking_3d(C, single_cpu, P, dims):
     halos), P processes through the tag-less FIFO staged transport."""
     r = torchrun(P, ["--backend", "hip", "--transport", "staged", "--shared-device"],
                  ARGS + ["--dims", dims])
-    assert r["dims"] == [int(x) for x in dims.split(",")] and r["kernel"] == "tb2"
+    assert r["dims"] == [int(x) for x in dims.split(",")] and r["kernel"] == "tb2r2w8"  # fp64 auto
     assert r["max_abs"] == single_cpu["max_abs"] and r["max_rel"] == single_cpu["max_rel"]
 
 

@@ -27,7 +27,7 @@ def test_golden_n32(C, kernel):
     from wave3d.utils import GOLDEN_N32_K20
 
     r = _solve(wave3d.WaveProblem(32, timesteps=20), kernel=kernel)
-    assert r.backend == "hip" and r.kernel == {"march": "march4", "auto": "tb2"}.get(kernel, kernel)
+    assert r.backend == "hip" and r.kernel == {"march": "march4", "auto": "tb2r2w8"}.get(kernel, kernel)
     assert _fmt(r) == GOLDEN_N32_K20
 
 
@@ -225,7 +225,7 @@ def test_temporal_blocking_3d_decomposition(C, dims, overlap):
         p = wave3d.WaveProblem(29, Lx=1.3, Ly="pi", Lz=2.0, timesteps=K, ic="shifted")
         base = _solve(p, backend="cpu", threads=4)
         r = _solve(p, ranks=P, dims=list(dims), overlap=overlap)
-        assert r.dims == list(dims) and r.kernel == "tb2"
+        assert r.dims == list(dims) and r.kernel == "tb2r2w8"  # fp64 auto
         assert r.max_abs == base.max_abs and r.max_rel == base.max_rel
 
 
