@@ -160,6 +160,67 @@ void k_step(const std::string& kind, bool first, uintptr_t u1, uintptr_t u2, uin
                    P<T>(tx), P<T>(ty), P<T>(tz), c, P<u64>(err), chunk, (hipStream_t)stream);
 }
 
+// Dense [nx][ny][nz] tensor with G ghost layers per side: logical (i,j,k) at tensor index
+// (i+G-1, j+G-1, k+G-1); returns the view and the logical-origin offset (elements).
+GridView gview_g(const std::vector<i64>& g, i64& origin) {
+    W3D_REQUIRE(g.size() == 4, "grid view = (nx, ny, nz, G)");
+    GridView v;
+    v.G = int(g[3]);
+    W3D_REQUIRE(v.G >= 1, "ghost depth >= 1");
+    v.X = int(g[0]) - 2 * v.G;
+    v.Y = int(g[1]) - 2 * v.G;
+    v.Z = int(g[2]) - 2 * v.G;
+    W3D_REQUIRE(v.X >= 1 && v.Y >= 1 && v.Z >= 1, "grid smaller than its ghosts");
+    v.sj = int(g[2]);
+    v.si = g[1] * g[2];
+    v.poff = (v.G - 1) * (v.sj + 1);
+    origin = i64(v.G - 1) * (v.si + v.sj + 1);
+    return v;
+}
+
+StepCoefs tocoefs(const std::vector<double>& c) {
+    W3D_REQUIRE(c.size() == 5, "coefs = (hx2, hy2, hz2, coef, ct)");
+    return StepCoefs{c[0], c[1], c[2], c[3], c[4]};
+}
+
+// One temporal-blocking sweep (k_tb2) on dense tensors: C = u^m, D = u^{m+1} from A, B.
+template <class T>
+void k_tb2_dense(int rows, int waves, bool first, uintptr_t A, uintptr_t B, uintptr_t Cc, uintptr_t D,
+                 const std::vector<i64>& g, const std::vector<std::vector<int>>& boxes,
+                 const std::vector<int>& cdom, int ei0, int ei1, const std::vector<int>& wrapC,
+                 const std::vector<int>& wrapD, uintptr_t tx, uintptr_t ty, uintptr_t tz,
+                 const std::vector<double>& cC, const std::vector<double>& cD, uintptr_t errC,
+                 uintptr_t errD, int chunk, uintptr_t stream) {
+    i64 o = 0;
+    const GridView v = gview_g(g, o);
+    W3D_REQUIRE(v.G >= 2, "k_tb2 needs ghost depth >= 2");
+    std::vector<Box> bx;
+    for (auto& b : boxes) bx.push_back(tobox(b));
+    launch_tb2<T>(rows, waves, 0, first, P<T>(A) + o, P<T>(B) + o, P<T>(Cc) + o, P<T>(D) + o, v,
+                  bx.data(), int(bx.size()), tobox(cdom), ei0, ei1, towrap(wrapC), towrap(wrapD),
+                  SeamAlias<T>{}, P<T>(tx), P<T>(ty), P<T>(tz), tocoefs(cC), tocoefs(cD),
+                  P<u64>(errC), P<u64>(errD), chunk, (hipStream_t)stream);
+}
+
+// One three-layer sweep (k_tb3): C = u^m (errors only), D = u^{m+1}, E = u^{m+2}.
+template <class T>
+void k_tb3_dense(int rows, int waves, bool first, uintptr_t A, uintptr_t B, uintptr_t D, uintptr_t E,
+                 const std::vector<i64>& g, const std::vector<std::vector<int>>& boxes,
+                 const std::vector<int>& cdom, int ei0, int ei1, uintptr_t tx, uintptr_t ty,
+                 uintptr_t tz, const std::vector<double>& cC, const std::vector<double>& cD,
+                 const std::vector<double>& cE, uintptr_t errC, uintptr_t errD, uintptr_t errE,
+                 int chunk, uintptr_t stream) {
+    i64 o = 0;
+    const GridView v = gview_g(g, o);
+    W3D_REQUIRE(v.G >= 3, "k_tb3 needs ghost depth >= 3");
+    std::vector<Box> bx;
+    for (auto& b : boxes) bx.push_back(tobox(b));
+    launch_tb3<T>(rows, waves, first, P<T>(A) + o, P<T>(B) + o, P<T>(D) + o, P<T>(E) + o, v,
+                  bx.data(), int(bx.size()), tobox(cdom), ei0, ei1, Wrap{}, Wrap{},
+                  SeamPartners<T>{}, P<T>(tx), P<T>(ty), P<T>(tz), tocoefs(cC), tocoefs(cD),
+                  tocoefs(cE), P<u64>(errC), P<u64>(errD), P<u64>(errE), chunk, (hipStream_t)stream);
+}
+
 template <class T>
 void k_init(uintptr_t u, const std::vector<i64>& g, const std::vector<int>& box,
             const std::vector<int>& wrap, uintptr_t tx, uintptr_t ty, uintptr_t tz, double ct0,
@@ -327,6 +388,13 @@ PYBIND11_MODULE(_wave3d_C, m) {
     // kernel-level entry points (device pointers as ints, explicit stream)
     m.def("k_step_f64", &k_step<double>);
     m.def("k_step_f32", &k_step<float>);
+    m.def("k_tb2_f64", &k_tb2_dense<double>);
+    m.def("k_tb2_f32", &k_tb2_dense<float>);
+    m.def("k_tb3_f64", &k_tb3_dense<double>);
+    m.def("k_tb3_f32", &k_tb3_dense<float>);
+    m.def("tb_supported", [](int depth, int rows, int waves) {
+        return depth == 3 ? tb3_supported(rows, waves) : tb2_supported(rows, waves, 0);
+    });
     m.def("k_init_f64", &k_init<double>);
     m.def("k_init_f32", &k_init<float>);
     m.def("k_faces_f64", &k_faces<double>);

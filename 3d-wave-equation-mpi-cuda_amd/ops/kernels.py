@@ -149,3 +149,77 @@ def faces(u, ops, to_buf: bool) -> None:
     if len(lst) > 4:
         raise ValueError("at most 4 faces per launch")
     getattr(_C(), "k_faces_" + _sfx(u))(u.data_ptr(), gv, lst, bool(to_buf), _stream())
+
+
+def _check_grid_g(G: int, *ts: torch.Tensor) -> list[int]:
+    """Dense [nx][ny][nz] grids with G ghost layers per side (logical 1..X owned)."""
+    u = ts[0]
+    for t in ts:
+        if not t.is_cuda or t.dim() != 3 or not t.is_contiguous():
+            raise ValueError("grids must be contiguous 3-D HIP device tensors")
+        if t.shape != u.shape or t.dtype != u.dtype:
+            raise ValueError("grid shapes/dtypes differ")
+    nx, ny, nz = u.shape
+    if min(nx, ny, nz) < 2 * G + 1:
+        raise ValueError(f"grid needs at least one owned node plus {G} ghosts per side")
+    return [nx, ny, nz, G]
+
+
+def _check_box_g(box, gv) -> list[int]:
+    i0, i1, j0, j1, k0, k1 = (int(v) for v in box)
+    X, Y, Z = (gv[a] - 2 * gv[3] for a in range(3))
+    if not (1 <= i0 <= i1 <= X and 1 <= j0 <= j1 <= Y and 1 <= k0 <= k1 <= Z):
+        raise ValueError(f"box {box} outside the owned region 1..{X} x 1..{Y} x 1..{Z}")
+    return [i0, i1, j0, j1, k0, k1]
+
+
+def tb_sweep(A, B, C, D, boxes, *, first: bool, cdom, err_i, tx, ty, tz, coefs_c, coefs_d,
+             err_c, err_d, rows: int = 2, waves: int = 4, chunk: int = 0, wrap_c=None,
+             wrap_d=None, ghost: int = 2) -> None:
+    """One temporal-blocking sweep (k_tb2): C = u^m and D = u^{m+1} on ``boxes`` from
+    A = u^{m-1}, B = u^{m-2} (dense grids with ``ghost`` >= 2 layers; logical indices).
+    ``cdom`` = (i0, i1, j0, j1, k0, k1): C is a stencil value inside it in j/k, 0 outside
+    (Dirichlet faces); coefs = (hx2, hy2, hz2, coef, ct) per layer."""
+    gv = _check_grid_g(ghost, A, B, C, D)
+    if ghost < 2:
+        raise ValueError("k_tb2 needs ghost depth >= 2")
+    if isinstance(boxes[0], int):
+        boxes = [boxes]
+    bl = [_check_box_g(b, gv) for b in boxes]
+    if not _C().tb_supported(2, rows, waves):
+        raise ValueError(f"unsupported tile rows={rows} waves={waves}")
+    for t in (tx, ty, tz):
+        if not t.is_cuda or t.dtype != A.dtype or t.numel() < max(gv[:3]):
+            raise ValueError("analytic tables must be device tensors covering the grid")
+    for e in (err_c, err_d):
+        if e.dtype != torch.int64 or e.numel() < 3 or not e.is_cuda:
+            raise ValueError("error slots must be >= 3 int64 device values (new_err())")
+    fn = getattr(_C(), "k_tb2_" + _sfx(A))
+    fn(int(rows), int(waves), bool(first), A.data_ptr(), B.data_ptr(), C.data_ptr(), D.data_ptr(),
+       gv, bl, [int(v) for v in cdom], int(err_i[0]), int(err_i[1]), list(wrap_c or []),
+       list(wrap_d or []), tx.data_ptr(), ty.data_ptr(), tz.data_ptr(),
+       [float(c) for c in coefs_c], [float(c) for c in coefs_d], err_c.data_ptr(),
+       err_d.data_ptr(), int(chunk), _stream())
+
+
+def tb3_sweep(A, B, D, E, boxes, *, first: bool, cdom, err_i, tx, ty, tz, coefs_c, coefs_d,
+              coefs_e, err_c, err_d, err_e, rows: int = 2, waves: int = 8, chunk: int = 0,
+              ghost: int = 3) -> None:
+    """One three-layer sweep (k_tb3): C = u^m (errors only), D = u^{m+1}, E = u^{m+2}."""
+    gv = _check_grid_g(ghost, A, B, D, E)
+    if ghost < 3:
+        raise ValueError("k_tb3 needs ghost depth >= 3")
+    if isinstance(boxes[0], int):
+        boxes = [boxes]
+    bl = [_check_box_g(b, gv) for b in boxes]
+    if not _C().tb_supported(3, rows, waves):
+        raise ValueError(f"unsupported tile rows={rows} waves={waves}")
+    for t in (tx, ty, tz):
+        if not t.is_cuda or t.dtype != A.dtype or t.numel() < max(gv[:3]):
+            raise ValueError("analytic tables must be device tensors covering the grid")
+    fn = getattr(_C(), "k_tb3_" + _sfx(A))
+    fn(int(rows), int(waves), bool(first), A.data_ptr(), B.data_ptr(), D.data_ptr(), E.data_ptr(),
+       gv, bl, [int(v) for v in cdom], int(err_i[0]), int(err_i[1]), tx.data_ptr(),
+       ty.data_ptr(), tz.data_ptr(), [float(c) for c in coefs_c], [float(c) for c in coefs_d],
+       [float(c) for c in coefs_e], err_c.data_ptr(), err_d.data_ptr(), err_e.data_ptr(),
+       int(chunk), _stream())

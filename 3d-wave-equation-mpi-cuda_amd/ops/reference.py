@@ -101,3 +101,29 @@ def solve(N: int, K: int, L=("pi", "pi", "pi"), T: float = 1.0, pi: str = "ref",
         abs_e.append(ma)
         rel_e.append(mr)
     return abs_e, rel_e, g[K % 3]
+
+
+def stencil_field(u1, u2, *, first: bool, hx2, hy2, hz2, coef) -> torch.Tensor:
+    """One layer on every node with a full 7-point neighbourhood: values for u1[1:-1, 1:-1, 1:-1]
+    (u2 unused when ``first``). The temporal-blocking oracle chains this per layer."""
+    lap = laplace7(u1, hx2, hy2, hz2)
+    c = u1[1:-1, 1:-1, 1:-1]
+    if first:
+        return c + coef * lap
+    return (2 * c - u2[1:-1, 1:-1, 1:-1]) + coef * lap
+
+
+def chained_layers(A, B, nlayers: int, *, first: bool, mask, hx2, hy2, hz2, coefs):
+    """Layers m, m+1, ... of a temporal-blocking sweep on full grids: C from (A, B), D from
+    (C, A), E from (D, C); each layer is 0 where ``mask`` is False (Dirichlet faces) and on the
+    outermost node ring of the grid (no stencil there)."""
+    out, prev2, prev1 = [], B, A
+    zero = torch.zeros((), dtype=A.dtype)
+    for q in range(nlayers):
+        v = torch.zeros_like(A)
+        val = stencil_field(prev1, prev2, first=first and q == 0, hx2=hx2, hy2=hy2, hz2=hz2,
+                            coef=coefs[q])
+        v[1:-1, 1:-1, 1:-1] = torch.where(mask[1:-1, 1:-1, 1:-1], val, zero)
+        out.append(v)
+        prev2, prev1 = prev1, v
+    return out

@@ -1,0 +1,167 @@
+"""Isolated temporal-blocking sweeps (k_tb2, k_tb3) vs the plain-PyTorch oracle.
+
+One launch on random fields: C = u^m and D = u^{m+1} (tb3: C errors only, D, E) over boxes
+that cross 64-lane k tiles, TJ-row j tiles and short i chunks, with a Dirichlet column inside
+the ring (C = 0 outside ``cdom``). The oracle chains ``reference.stencil_field`` per layer on
+the whole grid (ops/reference.py). fp64 must be bitwise equal (values and fused error
+maxima); fp32 within a few ulps (same rounded operations, reference on the CPU).
+The end-to-end solves are covered against the OpenMP oracle in test_gpu_solver.py.
+"""
+import math
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+COEF = dict(hx2=0.011, hy2=0.013, hz2=0.017)
+CT = (-0.83, 0.47, 0.21)
+COEFS = (3.1e-4, 2.9e-4, 2.7e-4)
+
+
+def _rand(shape, dtype, seed):
+    g = torch.Generator().manual_seed(seed)
+    return torch.rand(shape, generator=g, dtype=torch.float64).to(dtype)
+
+
+def _tables(n, dtype, seed):
+    g = torch.Generator().manual_seed(seed)
+    return [(torch.rand(n, generator=g, dtype=torch.float64) * 2 - 1).to(dtype) for _ in range(3)]
+
+
+def _mask(shape, G, cdom):
+    """j/k inside cdom (logical) as a tensor-index mask."""
+    m = torch.zeros(shape, dtype=torch.bool)
+    _, _, j0, j1, k0, k1 = cdom
+    m[:, j0 + G - 1:j1 + G, k0 + G - 1:k1 + G] = True
+    return m
+
+
+def _sl(box, G):
+    i0, i1, j0, j1, k0, k1 = box
+    o = G - 1
+    return (slice(i0 + o, i1 + o + 1), slice(j0 + o, j1 + o + 1), slice(k0 + o, k1 + o + 1))
+
+
+def _check(got, exp, dtype):
+    if dtype == torch.float64:
+        assert torch.equal(got, exp)
+    else:
+        torch.testing.assert_close(got, exp, rtol=4e-6, atol=4e-6)
+
+
+def _check_err(err, vals, box, ei, tx, ty, tz, ct, dtype):
+    from wave3d.ops import kernels, reference
+
+    i0, i1, j0, j1, k0, k1 = box
+    f = reference.analytic(tx[ei[0]:ei[1] + 1], ty[j0:j1 + 1], tz[k0:k1 + 1],
+                           torch.tensor(ct, dtype=dtype).item())
+    ea, er = reference.max_errors(vals[ei[0] - i0:ei[1] - i0 + 1].double(), f.double())
+    (ga, gr, bad), = kernels.decode_err(err)
+    if dtype == torch.float64:
+        assert ga == ea and gr == er
+    else:
+        assert math.isclose(ga, ea, rel_tol=1e-5) and math.isclose(gr, er, rel_tol=1e-4)
+    assert not bad
+
+
+CASES = [
+    # (X, Y, Z), boxes, cdom (j/k part used), chunk
+    ((9, 40, 131), [(2, 8, 3, 37, 60, 130)], (1, 9, 1, 40, 1, 130), 3),
+    ((9, 40, 131), [(1, 9, 1, 40, 1, 130)], (1, 9, 1, 40, 1, 130), 0),
+    ((12, 21, 70), [(1, 2, 1, 21, 1, 69), (3, 12, 5, 9, 2, 66)], (1, 12, 1, 21, 1, 69), 4),
+    ((7, 9, 11), [(1, 7, 2, 8, 2, 10)], (1, 7, 2, 8, 2, 10), 0),
+]
+
+
+@pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
+@pytest.mark.parametrize("first", [False, True])
+@pytest.mark.parametrize("rows,waves", [(2, 4), (2, 8), (4, 4)])
+@pytest.mark.parametrize("case", range(len(CASES)))
+def test_tb2_sweep_matches_reference(C, dtype, first, rows, waves, case):
+    from wave3d.ops import kernels, reference
+
+    (X, Y, Z), boxes, cdom, chunk = CASES[case]
+    G = 2
+    shape = (X + 2 * G, Y + 2 * G, Z + 2 * G)
+    A, B = _rand(shape, dtype, 1), _rand(shape, dtype, 2)
+    tx, ty, tz = _tables(max(shape), dtype, 3)
+    dA, dB, dC, dD = A.to(DEV), B.to(DEV), torch.full(shape, -7.0, dtype=dtype, device=DEV), \
+        torch.full(shape, -9.0, dtype=dtype, device=DEV)
+    errC, errD = kernels.new_err(1), kernels.new_err(1)
+    ei = (boxes[0][0], boxes[0][1])
+    if len(boxes) > 1:  # errors over every box's rows: use one shared i range
+        ei = (min(b[0] for b in boxes), max(b[1] for b in boxes))
+    kernels.tb_sweep(dA, dB, dC, dD, boxes, first=first, cdom=cdom, err_i=ei, tx=tx.to(DEV),
+                     ty=ty.to(DEV), tz=tz.to(DEV), coefs_c=(*COEF.values(), COEFS[0], CT[0]),
+                     coefs_d=(*COEF.values(), COEFS[1], CT[1]), err_c=errC, err_d=errD,
+                     rows=rows, waves=waves, chunk=chunk)
+    torch.cuda.synchronize()
+    cast = lambda v: torch.tensor(v, dtype=dtype).item()  # noqa: E731
+    h = {k: cast(v) for k, v in COEF.items()}
+    Cf, Df = reference.chained_layers(A, B, 2, first=first, mask=_mask(shape, G, cdom),
+                                      coefs=[cast(COEFS[0]), cast(COEFS[1])], **h)
+    gC, gD = dC.cpu(), dD.cpu()
+    touched = torch.zeros(shape, dtype=torch.bool)
+    for b in boxes:
+        s = _sl(b, G)
+        _check(gC[s], Cf[s], dtype)
+        _check(gD[s], Df[s], dtype)
+        touched[s] = True
+    assert bool((gC[~touched] == -7.0).all()) and bool((gD[~touched] == -9.0).all())
+    if len(boxes) == 1:
+        _check_err(errC, gC[_sl(boxes[0], G)], boxes[0], ei, tx, ty, tz, CT[0], dtype)
+        _check_err(errD, gD[_sl(boxes[0], G)], boxes[0], ei, tx, ty, tz, CT[1], dtype)
+
+
+@pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
+@pytest.mark.parametrize("first", [False, True])
+@pytest.mark.parametrize("rows,waves", [(2, 8), (2, 4)])
+@pytest.mark.parametrize("case", [0, 2, 3])
+def test_tb3_sweep_matches_reference(C, dtype, first, rows, waves, case):
+    from wave3d.ops import kernels, reference
+
+    (X, Y, Z), boxes, cdom, chunk = CASES[case]
+    G = 3
+    shape = (X + 2 * G, Y + 2 * G, Z + 2 * G)
+    A, B = _rand(shape, dtype, 4), _rand(shape, dtype, 5)
+    tx, ty, tz = _tables(max(shape), dtype, 6)
+    dD, dE = torch.full(shape, -7.0, dtype=dtype, device=DEV), torch.full(shape, -9.0, dtype=dtype, device=DEV)
+    errs = [kernels.new_err(1) for _ in range(3)]
+    ei = (min(b[0] for b in boxes), max(b[1] for b in boxes))
+    co = [(*COEF.values(), COEFS[q], CT[q]) for q in range(3)]
+    kernels.tb3_sweep(A.to(DEV), B.to(DEV), dD, dE, boxes, first=first, cdom=cdom, err_i=ei,
+                      tx=tx.to(DEV), ty=ty.to(DEV), tz=tz.to(DEV), coefs_c=co[0], coefs_d=co[1],
+                      coefs_e=co[2], err_c=errs[0], err_d=errs[1], err_e=errs[2], rows=rows,
+                      waves=waves, chunk=chunk)
+    torch.cuda.synchronize()
+    cast = lambda v: torch.tensor(v, dtype=dtype).item()  # noqa: E731
+    h = {k: cast(v) for k, v in COEF.items()}
+    Cf, Df, Ef = reference.chained_layers(A, B, 3, first=first, mask=_mask(shape, G, cdom),
+                                          coefs=[cast(c) for c in COEFS], **h)
+    gD, gE = dD.cpu(), dE.cpu()
+    for b in boxes:
+        s = _sl(b, G)
+        _check(gD[s], Df[s], dtype)
+        _check(gE[s], Ef[s], dtype)
+    if len(boxes) == 1:
+        s = _sl(boxes[0], G)
+        for err, vals, q in ((errs[0], Cf[s], 0), (errs[1], gD[s], 1), (errs[2], gE[s], 2)):
+            _check_err(err, vals, boxes[0], ei, tx, ty, tz, CT[q], dtype)
+
+
+def test_tb_sweep_shape_checks(C):
+    from wave3d.ops import kernels
+
+    G = 2
+    shape = (5 + 2 * G, 6 + 2 * G, 7 + 2 * G)
+    u = torch.zeros(shape, dtype=torch.float64, device=DEV)
+    t = torch.zeros(max(shape), dtype=torch.float64, device=DEV)
+    e = kernels.new_err(1)
+    kw = dict(first=False, cdom=(1, 5, 1, 6, 1, 7), err_i=(1, 5), tx=t, ty=t, tz=t,
+              coefs_c=(1, 1, 1, 1, 1), coefs_d=(1, 1, 1, 1, 1), err_c=e, err_d=e)
+    with pytest.raises(ValueError):
+        kernels.tb_sweep(u, u, u, u, (0, 5, 1, 6, 1, 7), **kw)   # i outside the owned region
+    with pytest.raises(ValueError):
+        kernels.tb_sweep(u, u, u, u, (1, 5, 1, 6, 1, 7), rows=3, waves=4, **kw)  # no such tile
