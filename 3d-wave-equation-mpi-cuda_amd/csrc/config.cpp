@@ -11,6 +11,7 @@ std::string usage() {
            "options:\n"
            "  --dtype fp64|fp32      compute precision (default fp64)\n"
            "  --pi ref|exact         ref = 3.1415926535 as the reference CPU programs (default)\n"
+           "  --scheme leapfrog|delta  delta = increment form (fp32 accuracy; tb2 kernels, CPU)\n"
            "  --ic ref|shifted       shifted = sin(2*pi*x/Lx + 0.7) periodic-BC check\n"
            "  --dims a,b,c           override the Cartesian process grid\n"
            "  --ranks P              simulate P ranks in-process (loopback transport)\n"
@@ -101,6 +102,11 @@ Config parse_cli(const std::vector<std::string>& a) {
             if (v == "fp64" || v == "f64" || v == "double") c.dtype = DType::F64;
             else if (v == "fp32" || v == "f32" || v == "float") c.dtype = DType::F32;
             else throw Error("wave3d: bad --dtype " + v);
+        } else if (o == "--scheme") {
+            const std::string& v = need(i++);
+            if (v == "leapfrog") c.delta = false;
+            else if (v == "delta") c.delta = true;
+            else throw Error("wave3d: bad --scheme " + v);
         } else if (o == "--pi") {
             const std::string& v = need(i++);
             if (v == "ref") c.pi = PiMode::Ref;
@@ -189,6 +195,8 @@ Config parse_cli(const std::vector<std::string>& a) {
         }
     }
     W3D_REQUIRE(c.repeat >= 1 && c.warmup >= 0, "bad --repeat/--warmup");
+    W3D_REQUIRE(!c.delta || (c.checkpoint_every == 0 && c.resume_dir.empty()),
+                "--scheme delta does not support checkpoints yet");
     W3D_REQUIRE(c.checkpoint_every == 0 || !c.checkpoint_dir.empty(),
                 "--checkpoint-every needs --checkpoint-dir");
     if (c.fault.empty()) {

@@ -27,6 +27,9 @@ struct Config {
 
     // extensions
     DType dtype = DType::F64;
+    bool delta = false;             // --scheme delta: increment form u^n = u^{n-1} + d^n,
+                                    // d^n = d^{n-1} + a2 tau^2 lap u^{n-1} (same scheme in exact
+                                    // arithmetic; no 2u - u cancellation, fp32 accuracy)
     PiMode pi = PiMode::Ref;
     ICMode ic = ICMode::Ref;
     int dims[3] = {0, 0, 0};        // 0 = let dims_create choose (MPI_Dims_create semantics)

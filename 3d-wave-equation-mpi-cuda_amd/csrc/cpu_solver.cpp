@@ -121,6 +121,7 @@ public:
         res.kernel = "openmp";
         res.transport = ext_ ? ext_->name() : (world_ > 1 ? "loopback" : "self");
         res.comm_size = ext_ ? ext_->comm_size() : 0;
+        res.scheme = cfg_.delta ? "delta" : "leapfrog";
         res.courant = prob_.courant;
         for (int a = 0; a < 3; ++a) res.dims[a] = ranks_[0].topo.dims[a];
         Timings t;
@@ -222,10 +223,15 @@ private:
         }
     }
 
+    // Leapfrog: u^n -> slot n%3 from u^{n-1} (slot (n+2)%3) and u^{n-2} (slot (n+1)%3).
+    // Increment form (--scheme delta): d^{n-1} lives in slot n%3, so d^n = d^{n-1} + coef*lap
+    // and u^n = u^{n-1} + d^n are formed point by point, u^n overwriting d^{n-1} in place and
+    // d^n going to slot (n+1)%3 (u^{n-2}, no longer needed); halos and wraps concern u only.
     void step(RankState<T>& R, int n) {
         const T* u1 = R.g[(n + 2) % 3].data();
         const T* u2 = R.g[(n + 1) % 3].data();
         T* u = R.g[n % 3].data();
+        T* dnext = cfg_.delta ? R.g[(n + 1) % 3].data() : nullptr;
         Box cb = R.topo.compute_box();
         Box eb = R.topo.error_box();
         const T hx2 = T(prob_.hx2), hy2 = T(prob_.hy2), hz2 = T(prob_.hz2);
@@ -249,7 +255,14 @@ private:
                         const T c = u1[p];
                         T lap = laplace7(c, u1[p - si], u1[p + si], u1[p - sj], u1[p + sj],
                                          u1[p - 1], u1[p + 1], hx2, hy2, hz2);
-                        T v = first ? taylor_first(c, lap, coef1) : leapfrog(c, u2[p], lap, coef);
+                        T v;
+                        if (dnext) {
+                            const T d = first ? coef1 * lap : delta_incr(u[p], lap, coef);
+                            v = c + d;
+                            dnext[p] = d;
+                        } else {
+                            v = first ? taylor_first(c, lap, coef1) : leapfrog(c, u2[p], lap, coef);
+                        }
                         u[p] = v;
                         lb |= nonfinite(v);
                         if (erow) accumulate_error(v, analytic(R.tx[i], R.ty[j], R.tz[k], cn), la, lr);

@@ -34,6 +34,7 @@ namespace {
 template <class T>
 struct StepParams {
     int xcd;  // XCD-aware tile order (xcd_swizzle)
+    int delta;  // increment form (k_naive / k_flat): u2 holds d^{n-1}, u = u1 + (u2 + coef lap)
     const T* u1;
     const T* u2;
     T* u;
@@ -321,7 +322,8 @@ __global__ void __launch_bounds__(kThreads) k_naive(const StepParams<T> p) {
             const T lap = laplace7_cr(c, p.u1[o - si], p.u1[o + si], p.u1[o - p.sj],
                                       p.u1[o + p.sj], p.u1[o - 1], p.u1[o + 1], p.hx2, p.hy2,
                                       p.hz2, p.yx2, p.yy2, p.yz2);
-            const T v = FIRST ? taylor_first(c, lap, p.coef) : leapfrog(c, p.u2[o], lap, p.coef);
+            const T v = FIRST ? taylor_first(c, lap, p.coef)
+                        : (p.delta ? c + delta_incr(p.u2[o], lap, p.coef) : leapfrog(c, p.u2[o], lap, p.coef));
             store_point(p, i, j, k, o, rowoff, v);
             chk += v;
             if (i >= p.ei0 && i <= p.ei1)
@@ -358,7 +360,8 @@ __global__ void __launch_bounds__(kThreads) k_flat(const StepParams<T> p) {
         const T lap = laplace7_cr(c, p.u1[o - si], p.u1[o + si], p.u1[o - p.sj], p.u1[o + p.sj],
                                   p.u1[o - 1], p.u1[o + 1], p.hx2, p.hy2, p.hz2, p.yx2, p.yy2,
                                   p.yz2);
-        const T v = FIRST ? taylor_first(c, lap, p.coef) : leapfrog(c, p.u2[o], lap, p.coef);
+        const T v = FIRST ? taylor_first(c, lap, p.coef)
+                    : (p.delta ? c + delta_incr(p.u2[o], lap, p.coef) : leapfrog(c, p.u2[o], lap, p.coef));
         store_point(p, i, j, k, o, rowoff, v);
         chk += v;
         if (i >= p.ei0 && i <= p.ei1) accumulate_error_dev(v, analytic(p.tx[i], p.ty[j], p.tz[k], p.ct), ma, mr);
@@ -545,6 +548,8 @@ void launch_step(const KernelVariant& kind, bool first, const T* u1, const T* u2
     W3D_REQUIRE(nbox >= 1 && nbox <= kMaxBoxes, "bad box count");
     StepParams<T> p{};
     p.xcd = xcd_swizzle_enabled();
+    p.delta = kind.delta ? 1 : 0;
+    W3D_REQUIRE(!kind.delta || !kind.march || kind.flat, "increment form: naive or flat kernel only");
     p.u1 = u1;
     p.u2 = u2;
     p.u = u;

@@ -63,6 +63,7 @@ struct KernelVariant {
     bool fast = false;  // reciprocal/FMA math: not bitwise-reproducible (benchmark ablation)
     bool pk = false;    // packed fp32: two rows per v_pk_* instruction (fp32 only)
     bool flat = false;  // one point per thread over the flattened boxes (thin overlap shells)
+    bool delta = false; // increment form: u2 holds d^{n-1} (naive / flat kernels only)
 };
 KernelVariant parse_kernel_variant(const std::string& name);
 std::string kernel_variant_name(const KernelVariant& v);
@@ -173,8 +174,11 @@ struct SeamAlias {
 // `rows` per lane x `waves` wave64s per workgroup = tile height (tb2_supported()).
 // `occ` > 0 caps registers so that many waves fit per SIMD (may spill a little).
 bool tb2_supported(int rows, int waves, int occ = 0);
+// delta: increment form — B holds d^{m-1}; C receives d^{m+1} (planes of D, with C's wrap
+// planes), D receives u^{m+1}; u^m is formed in registers for its errors only.
+bool tb2_delta_supported(int rows, int waves);
 template <class T>
-void launch_tb2(int rows, int waves, int occ, bool first, const T* A, const T* B, T* C, T* D, const GridView& gv,
+void launch_tb2(int rows, int waves, int occ, bool delta, bool first, const T* A, const T* B, T* C, T* D, const GridView& gv,
                 const Box* boxes, int nbox, const Box& cdom, int ei0, int ei1, const Wrap& wrapC,
                 const Wrap& wrapD, const SeamAlias<T>& alias, const T* tx, const T* ty,
                 const T* tz, const StepCoefs& cC, const StepCoefs& cD, u64* errC, u64* errD,

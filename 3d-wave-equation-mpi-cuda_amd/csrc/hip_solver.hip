@@ -132,6 +132,16 @@ public:
         kind_ = parse_kernel_variant(tb_ ? std::string("auto") : c.kernel);
         naive_.march = false;
         naive_.flat = true;  // thin overlap shells: flattened one-point-per-thread kernel
+        if (c.delta) {
+            // increment form: temporal blocking sweeps (u and d levels in the ring: after a
+            // sweep, lvl(m+1) = u^{m+1}, lvl(m) = d^{m+1}); an odd last layer is one step of
+            // the naive/flat kernel reading that d level
+            W3D_REQUIRE(tb_ && tbd_ == 2, "--scheme delta needs a tb2 kernel (kernel auto or tb2*)");
+            kind_ = KernelVariant{};
+            kind_.march = false;
+            kind_.delta = true;
+            naive_.delta = true;
+        }
         // interior/shell split + comm stream whenever there is a remote halo to hide
         overlap_ = c.overlap && (ext_ != nullptr || world_ > 1);
         // test mode: the periodic x wrap of a dims[0] == 1 rank goes through the transport as
@@ -193,6 +203,7 @@ public:
         res.courant = prob_.courant;
         res.transport = ext_ ? ext_->name() : (world_ > 1 ? "loopback" : "self");
         res.overlap = overlap_;
+        res.scheme = cfg_.delta ? "delta" : "leapfrog";
         res.comm_size = ext_ ? ext_->comm_size() : 0;
         for (int a = 0; a < 3; ++a) res.dims[a] = ranks_[0].topo.dims[a];
         Timings t;
@@ -211,6 +222,7 @@ public:
     std::vector<FieldBlock> field(int layer) {
         const int K = prob_.K;
         W3D_REQUIRE(layer >= std::max(0, K - 1) && layer <= K, "field: only layers K-1 and K are kept");
+        W3D_REQUIRE(!cfg_.delta || layer == K, "field: the increment form keeps only layer K");
         HIP_CHECK(hipDeviceSynchronize());
         std::vector<FieldBlock> out;
         for (auto& R : ranks_) {
@@ -695,7 +707,7 @@ private:
             al.prev = R.alias_buf + R.plane_off;
         }
         if (!boxes) boxes = &R.compute, nbox = 1;
-        launch_tb2<T>(tb_rows_, tb_waves_, tb_occ_, m == 1, A, B, R.g[lvl(m)], R.g[lvl(m + 1)], R.gv, boxes, nbox,
+        launch_tb2<T>(tb_rows_, tb_waves_, tb_occ_, cfg_.delta, m == 1, A, B, R.g[lvl(m)], R.g[lvl(m + 1)], R.gv, boxes, nbox,
                       R.cdom, R.error.i0, R.error.i1, R.wrap, R.wrap2, al, R.tx, R.ty, R.tz,
                       coefs(m), coefs(m + 1), R.err + size_t(m) * kSlotsPerLayer,
                       R.err + size_t(m + 1) * kSlotsPerLayer, cfg_.chunk, s);

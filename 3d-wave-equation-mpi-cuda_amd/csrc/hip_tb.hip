@@ -73,7 +73,10 @@ struct TbParams {
 // profiles/sweep_tb2_cache_policy_r1.txt). OPT (env WAVE3D_TB_OPT, A/B ablation, bitwise-
 // neutral): 1 = default-policy stores instead. (Prefetch distances: own A and both A rings 2
 // planes, B 1 plane; B at distance 2 measured no faster, the outer ring at distance 2 +2.6 %.)
-template <class T, bool FIRST, int R, int NW, int WPE = 1, int ABL = 0, int OPT = 0>
+// DELTA: increment form (csrc/hip_kernels.hpp launch_tb2): B = d^{m-1}; d^m = B + coefC*lap A,
+// C = A + d^m (registers: errors, D's stencil); d^{m+1} = d^m + coefD*lap C, D = C + d^{m+1};
+// the C level receives d^{m+1} at D's planes, so the store count is unchanged.
+template <class T, bool FIRST, int R, int NW, int WPE = 1, int ABL = 0, int OPT = 0, bool DELTA = false>
 __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WPE, 8))) k_tb2(const TbParams<T> p) {
     constexpr int TJ = NW * R;
     constexpr int AH = TJ + 4, AW = kTK + 4;  // A tile: rows jt-2..jt+TJ+1, cols kb-2..kb+65
@@ -159,6 +162,7 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WP
     //   C(x):            slot (x - ib + 1) & 3 -> C(i) = P, C(i-1) = P+3, C(i-2) = P+2
     //   B(x), ring B(x), LDS buffer: (x - ib + 1) & 1
     T a[4][R], c[4][R], bb[2][R];
+    T dl[DELTA ? 2 : 1][R];  // increment form: d^m of planes i (H0) and i-1 (H1)
     T ra[4], rb[2], ua[4];
     {
         const auto r0 = prs(p.A, ib - 2), r1 = prs(p.A, ib - 1), r2 = prs(p.A, ib);
@@ -252,8 +256,15 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WP
                                       ldsA[H0][ya + 1][xa], ldsA[H0][ya][xa - 1],
                                       ldsA[H0][ya][xa + 1], p.hx2, p.hy2, p.hz2, p.yx2, p.yy2,
                                       p.yz2);
-            const T cv = FIRST ? taylor_first(a[S1][r], lap, p.coefC)
-                               : leapfrog(a[S1][r], bb[H0][r], lap, p.coefC);
+            T cv;
+            if constexpr (DELTA) {
+                const T dm = FIRST ? p.coefC * lap : delta_incr(bb[H0][r], lap, p.coefC);
+                dl[H0][r] = ocd[r] ? dm : T(0);
+                cv = a[S1][r] + dm;  // FIRST: = taylor_first (u0 + coef_first*lap)
+            } else {
+                cv = FIRST ? taylor_first(a[S1][r], lap, p.coefC)
+                           : leapfrog(a[S1][r], bb[H0][r], lap, p.coefC);
+            }
             c[S0][r] = ocd[r] ? cv : T(0);
             ldsC[H0][1 + w * R + r][1 + lane] = c[S0][r];
         }
@@ -263,7 +274,8 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WP
                                       ldsA[H0][ya][xa - 1], ldsA[H0][ya][xa + 1], p.hx2, p.hy2,
                                       p.hz2, p.yx2, p.yy2, p.yz2);
             const T cv = FIRST ? taylor_first(ra[S1], lap, p.coefC)
-                               : leapfrog(ra[S1], rb[H0], lap, p.coefC);
+                               : (DELTA ? ra[S1] + delta_incr(rb[H0], lap, p.coefC)
+                                        : leapfrog(ra[S1], rb[H0], lap, p.coefC));
             ldsC[H0][ya - 1][xa - 1] = rcd ? cv : T(0);
         }
 
@@ -271,10 +283,11 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WP
         if (i >= ib && i <= ie) {
             const auto rc = prs(p.C, i);
 #pragma unroll
-            for (int r = 0; r < R; ++r) bst<kStAux>(c[S0][r], rc, os[r]);
+            for (int r = 0; r < R; ++r)
+                if constexpr (!DELTA) bst<kStAux>(c[S0][r], rc, os[r]);
 #pragma unroll
             for (int g = 0; g < 2; ++g)
-                if (i >= p.wc_lo[g] && i <= p.wc_hi[g]) {
+                if (!DELTA && i >= p.wc_lo[g] && i <= p.wc_hi[g]) {
                     const auto rw = prs(p.C, i + p.wc_sh[g]);
 #pragma unroll
                     for (int r = 0; r < R; ++r) bst<kStAux>(c[S0][r], rw, os[r]);
@@ -306,11 +319,28 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WP
                                           ldsC[H1][yc + 1][xc], ldsC[H1][yc][xc - 1],
                                           ldsC[H1][yc][xc + 1], p.hx2, p.hy2, p.hz2, p.yx2,
                                           p.yy2, p.yz2);
-                dv[r] = leapfrog(c[S3][r], a[S0][r], lap, p.coefD);
+                if constexpr (DELTA) {
+                    dl[H1][r] = delta_incr(dl[H1][r], lap, p.coefD);  // d^{m+1}
+                    dv[r] = c[S3][r] + dl[H1][r];
+                } else {
+                    dv[r] = leapfrog(c[S3][r], a[S0][r], lap, p.coefD);
+                }
             }
             const auto rd = prs(p.D, id);
 #pragma unroll
             for (int r = 0; r < R; ++r) bst<kStAux>(dv[r], rd, os[r]);
+            if constexpr (DELTA) {
+                const auto rdc = prs(p.C, id);
+#pragma unroll
+                for (int r = 0; r < R; ++r) bst<kStAux>(dl[H1][r], rdc, os[r]);
+#pragma unroll
+                for (int g = 0; g < 2; ++g)
+                    if (id >= p.wc_lo[g] && id <= p.wc_hi[g]) {
+                        const auto rw = prs(p.C, id + p.wc_sh[g]);
+#pragma unroll
+                        for (int r = 0; r < R; ++r) bst<kStAux>(dl[H1][r], rw, os[r]);
+                    }
+            }
 #pragma unroll
             for (int g = 0; g < 2; ++g)
                 if (id >= p.wd_lo[g] && id <= p.wd_hi[g]) {
@@ -361,6 +391,19 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WP
 
 }  // namespace
 
+// increment form: the main tile shapes only
+template <class T, bool F>
+static void (*tb_delta_kernel(int rows, int waves))(const TbParams<T>) {
+    switch (rows * 10 + waves) {
+        case 24: return k_tb2<T, F, 2, 4, 1, 0, 0, true>;
+        case 28: return k_tb2<T, F, 2, 8, 1, 0, 0, true>;
+        case 44: return k_tb2<T, F, 4, 4, 1, 0, 0, true>;
+        default: return nullptr;
+    }
+}
+
+bool tb2_delta_supported(int rows, int waves) { return tb_delta_kernel<double, false>(rows, waves) != nullptr; }
+
 // rows x waves (x minimum waves per SIMD: register cap for the compiler, 0 = none)
 template <class T, bool F>
 static void (*tb_kernel(int rows, int waves, int occ))(const TbParams<T>) {
@@ -396,13 +439,15 @@ bool tb2_supported(int rows, int waves, int occ) {
 }
 
 template <class T>
-void launch_tb2(int rows, int waves, int occ, bool first, const T* A, const T* B, T* C, T* D, const GridView& gv,
+void launch_tb2(int rows, int waves, int occ, bool delta, bool first, const T* A, const T* B, T* C, T* D, const GridView& gv,
                 const Box* boxes, int nbox, const Box& cdom, int ei0, int ei1, const Wrap& wrapC,
                 const Wrap& wrapD, const SeamAlias<T>& alias, const T* tx, const T* ty,
                 const T* tz, const StepCoefs& cC, const StepCoefs& cD, u64* errC, u64* errD,
                 int chunk, hipStream_t s) {
     W3D_REQUIRE(gv.G >= 2, "temporal blocking needs ghost depth >= 2");
     W3D_REQUIRE(tb2_supported(rows, waves, occ), "tb2: unsupported rows x waves x occupancy");
+    W3D_REQUIRE(!delta || (occ == 0 && tb2_delta_supported(rows, waves)),
+                "tb2 increment form: tiles r2w4, r2w8, r4w4 only");
     W3D_REQUIRE(nbox >= 1 && nbox <= kMaxBoxes, "bad box count");
     TbParams<T> p{};
     p.xcd = xcd_swizzle_enabled();
@@ -468,13 +513,14 @@ void launch_tb2(int rows, int waves, int occ, bool first, const T* A, const T* B
     }
     p.nbox = nb;
     if (nb == 0) return;
-    auto kern = first ? tb_kernel<T, true>(rows, waves, occ) : tb_kernel<T, false>(rows, waves, occ);
+    auto kern = delta ? (first ? tb_delta_kernel<T, true>(rows, waves) : tb_delta_kernel<T, false>(rows, waves))
+                      : (first ? tb_kernel<T, true>(rows, waves, occ) : tb_kernel<T, false>(rows, waves, occ));
     hipLaunchKernelGGL(kern, dim3(total), dim3(waves * 64), 0, s, p);
     HIP_OK(hipGetLastError());
 }
 
 #define W3D_TB_INST(T)                                                                       \
-    template void launch_tb2<T>(int, int, int, bool, const T*, const T*, T*, T*, const GridView&,      \
+    template void launch_tb2<T>(int, int, int, bool, bool, const T*, const T*, T*, T*, const GridView&, \
                                 const Box*, int, const Box&, int, int, const Wrap&,          \
                                 const Wrap&, const SeamAlias<T>&, const T*, const T*,        \
                                 const T*, const StepCoefs&, const StepCoefs&, u64*, u64*,    \

@@ -91,7 +91,8 @@ std::string json_summary(const Config& c, const RunResult& r) {
     s << "{\"N\": " << r.N << ", \"timesteps\": " << r.K << ", \"nprocs\": " << r.nprocs
       << ", \"dims\": [" << r.dims[0] << ", " << r.dims[1] << ", " << r.dims[2] << "]"
       << ", \"dtype\": \"" << dtype_name(r.dtype) << "\", \"backend\": \"" << r.backend
-      << "\", \"kernel\": \"" << r.kernel << "\", \"transport\": \"" << r.transport << "\""
+      << "\", \"kernel\": \"" << r.kernel << "\", \"scheme\": \"" << r.scheme
+      << "\", \"transport\": \"" << r.transport << "\""
       << ", \"overlap\": " << (r.overlap ? "true" : "false")
       << ", \"comm_size\": " << r.comm_size
       << ", \"courant\": " << jnum(r.courant) << ", \"total_ms\": " << jnum(r.t.total_ms)

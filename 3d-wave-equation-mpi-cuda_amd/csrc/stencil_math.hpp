@@ -42,6 +42,16 @@ W3D_HD T leapfrog(T c, T u2, T lap, T coef) {
     return (T(2) * c - u2) + coef * lap;
 }
 
+// Increment form: d^n = d^{n-1} + coef*lap, u^n = u^{n-1} + d^n (the same scheme as
+// leapfrog in exact arithmetic, without the 2u - u cancellation). Returns d^n; u^n = c + d^n.
+template <class T>
+W3D_HD T delta_incr(T d, T lap, T coef) {
+#ifdef __clang__
+#pragma clang fp contract(off)
+#endif
+    return d + coef * lap;
+}
+
 template <class T>
 W3D_HD T taylor_first(T c, T lap, T coef_first) {
 #ifdef __clang__

@@ -34,6 +34,7 @@ class WaveProblem:
     dtype: str = "fp64"
     pi: str = "ref"
     ic: str = "ref"
+    scheme: str = "leapfrog"  # "delta": increment form (u^n = u^{n-1} + d^n), fp32 accuracy
 
     def _pi(self) -> float:
         return PI_REF if self.pi == "ref" else math.pi
@@ -65,7 +66,7 @@ class WaveProblem:
     def args(self, Np: int = 1, **opts) -> list[str]:
         a = [str(self.N), str(Np), _len_arg(self.Lx), _len_arg(self.Ly), _len_arg(self.Lz),
              repr(float(self.T)), str(self.timesteps),
-             "--dtype", self.dtype, "--pi", self.pi, "--ic", self.ic]
+             "--dtype", self.dtype, "--pi", self.pi, "--ic", self.ic, "--scheme", self.scheme]
         for k, v in opts.items():
             if v is None or v is False:
                 continue

@@ -69,10 +69,11 @@ def tables(N: int, K: int, L=("pi", "pi", "pi"), T: float = 1.0, pi: str = "ref"
 
 
 def solve(N: int, K: int, L=("pi", "pi", "pi"), T: float = 1.0, pi: str = "ref",
-          phase: float = 0.0, dtype=torch.float64, device="cpu"):
+          phase: float = 0.0, dtype=torch.float64, device="cpu", scheme: str = "leapfrog"):
     """Whole single-domain solve in PyTorch; returns (max_abs[0..K], max_rel[0..K], u_K).
 
     Storage: x has ghost planes (local = global + 1), y/z none (faces are Dirichlet).
+    scheme "delta": increment form, d^n = d^{n-1} + coef*lap u^{n-1}, u^n = u^{n-1} + d^n.
     """
     sx, sy, sz, ct, c = tables(N, K, L, T, pi, phase, dtype)
     sx, sy, sz = sx.to(device), sy.to(device), sz.to(device)
@@ -87,13 +88,20 @@ def solve(N: int, K: int, L=("pi", "pi", "pi"), T: float = 1.0, pi: str = "ref",
     wrap(g[0])
     ma, mr = max_errors(f0, f0)
     abs_e, rel_e = [ma], [mr]
+    d = None
     for n in range(1, K + 1):
         u1, u2, u = g[(n + 2) % 3], g[(n + 1) % 3], g[n % 3]
         u.zero_()
         # stencil points: all x (incl. the periodic planes), y/z global 1..N-1
         box = (1, N + 1, 1, N - 1, 1, N - 1)
-        vals = step(u1, u2, box, first=n == 1, hx2=c["hx2"], hy2=c["hy2"], hz2=c["hz2"],
-                    coef=c["coef_first"] if n == 1 else c["coef"])
+        coef = c["coef_first"] if n == 1 else c["coef"]
+        if scheme == "delta":
+            lap = laplace7(u1, c["hx2"], c["hy2"], c["hz2"])[0:N + 1, 0:N - 1, 0:N - 1]
+            d = coef * lap if n == 1 else d + coef * lap
+            vals = u1[1:N + 2, 1:N, 1:N] + d
+        else:
+            vals = step(u1, u2, box, first=n == 1, hx2=c["hx2"], hy2=c["hy2"], hz2=c["hz2"],
+                        coef=coef)
         u[1:N + 2, 1:N, 1:N] = vals
         wrap(u)
         f = analytic(sx[1:N], sy[1:N], sz[1:N], ct[n])
@@ -111,6 +119,27 @@ def stencil_field(u1, u2, *, first: bool, hx2, hy2, hz2, coef) -> torch.Tensor:
     if first:
         return c + coef * lap
     return (2 * c - u2[1:-1, 1:-1, 1:-1]) + coef * lap
+
+
+def chained_delta(A, Dm1, *, first: bool, mask, hx2, hy2, hz2, coefs):
+    """Increment-form sweep oracle (k_tb2 delta): d^m = d^{m-1} + c0*lap A (c0*lap A when
+    ``first``), C = A + d^m, d^{m+1} = d^m + c1*lap C, D = C + d^{m+1}; C and d are 0 where
+    ``mask`` is False. Returns (C, D, d^{m+1}) on the full grid."""
+    zero = torch.zeros((), dtype=A.dtype)
+    inner = (slice(1, -1),) * 3
+
+    def lap_of(u):
+        v = torch.zeros_like(u)
+        v[inner] = laplace7(u, hx2, hy2, hz2)
+        return v
+    m = mask.clone()
+    m[0], m[-1], m[:, 0], m[:, -1], m[:, :, 0], m[:, :, -1] = (False,) * 6
+    la = lap_of(A)
+    dm = coefs[0] * la if first else Dm1 + coefs[0] * la
+    dm = torch.where(m, dm, zero)
+    Cf = torch.where(m, A + dm, zero)
+    dn = dm + coefs[1] * lap_of(Cf)
+    return Cf, Cf + dn, dn
 
 
 def chained_layers(A, B, nlayers: int, *, first: bool, mask, hx2, hy2, hz2, coefs):

@@ -70,6 +70,33 @@ def test_bitwise_equal_to_torch_reference(C):
         assert r.max_abs == a and r.max_rel == b
 
 
+def test_delta_scheme_bitwise_equal_to_torch_reference(C):
+    """Increment form (--scheme delta) of the OpenMP oracle == the PyTorch delta solve."""
+    import wave3d
+    from wave3d.ops import reference
+
+    for ic, phase in (("ref", 0.0), ("shifted", 0.7)):
+        r = _solve(wave3d.WaveProblem(24, Lx=1.1, Ly="pi", Lz=1.9, timesteps=9, ic=ic, scheme="delta"))
+        a, b, _ = reference.solve(24, 9, L=(1.1, "pi", 1.9), phase=phase, scheme="delta")
+        assert r.max_abs == a and r.max_rel == b and r.extra["scheme"] == "delta"
+        # decomposition invariance holds for the increment form too
+        m = _solve(wave3d.WaveProblem(24, Lx=1.1, Ly="pi", Lz=1.9, timesteps=9, ic=ic, scheme="delta"),
+                   ranks=4)
+        assert m.max_abs == r.max_abs and m.max_rel == r.max_rel
+
+
+def test_delta_scheme_fp32_accuracy(C):
+    """fp32 with the increment form stays at the fp64 error (the leapfrog's 2u - u cancellation
+    is gone); plain fp32 leapfrog is ~80x worse here (N=128, K=400)."""
+    import wave3d
+
+    p = dict(timesteps=400)
+    e64 = _solve(wave3d.WaveProblem(128, **p)).max_abs[-1]
+    lf32 = _solve(wave3d.WaveProblem(128, dtype="fp32", **p)).max_abs[-1]
+    d32 = _solve(wave3d.WaveProblem(128, dtype="fp32", scheme="delta", **p)).max_abs[-1]
+    assert d32 < 1.2 * e64 and lf32 > 20 * d32
+
+
 def test_fp32_close_to_fp64(C):
     import wave3d
 

@@ -299,3 +299,33 @@ def test_field_bitwise_vs_cpu(C, kernel, ranks, layer):
     _, ref = wave3d.WaveSolver(p, "cpu", threads=4).solve_field(layer)
     _, got = wave3d.WaveSolver(p, "hip", kernel=kernel, ranks=ranks).solve_field(layer)
     assert np.array_equal(got, ref)
+
+
+@pytest.mark.parametrize("dtype", ["fp64", "fp32"])
+@pytest.mark.parametrize("kernel,ranks,dims,overlap", [
+    ("auto", 0, None, True), ("tb2", 0, None, True), ("tb2r4", 0, None, True),
+    ("auto", 2, [2, 1, 1], True), ("tb2", 3, [3, 1, 1], False), ("auto", 8, [2, 2, 2], True),
+    ("tb2", 4, [1, 2, 2], False)])
+def test_delta_scheme_matches_cpu(C, dtype, kernel, ranks, dims, overlap):
+    """Increment form on the HIP temporal-blocking path (u and d levels in the ring, an odd last
+    layer as one naive/flat step) == the OpenMP oracle's increment form, bit for bit, for even
+    and odd K, one rank, x slabs and 3-D blocks, with and without the overlap."""
+    import wave3d
+
+    for K in (10, 11):
+        p = wave3d.WaveProblem(29, Lx=1.3, Ly="pi", Lz=2.0, timesteps=K, ic="shifted", dtype=dtype,
+                               scheme="delta")
+        ref = _solve(p, backend="cpu", threads=4)
+        got = _solve(p, kernel=kernel, ranks=ranks, dims=dims, overlap=overlap)
+        assert got.extra["scheme"] == "delta"
+        assert got.max_abs == ref.max_abs and got.max_rel == ref.max_rel
+
+
+def test_delta_scheme_fp32_accuracy_gpu(C):
+    """fp32 increment form at the fp64 error where fp32 leapfrog is far off (N=128, K=400)."""
+    import wave3d
+
+    e64 = _solve(wave3d.WaveProblem(128, timesteps=400)).linf_abs
+    lf = _solve(wave3d.WaveProblem(128, timesteps=400, dtype="fp32")).linf_abs
+    d = _solve(wave3d.WaveProblem(128, timesteps=400, dtype="fp32", scheme="delta")).linf_abs
+    assert d < 1.2 * e64 and lf > 20 * d

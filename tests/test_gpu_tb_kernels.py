@@ -165,3 +165,41 @@ def test_tb_sweep_shape_checks(C):
         kernels.tb_sweep(u, u, u, u, (0, 5, 1, 6, 1, 7), **kw)   # i outside the owned region
     with pytest.raises(ValueError):
         kernels.tb_sweep(u, u, u, u, (1, 5, 1, 6, 1, 7), rows=3, waves=4, **kw)  # no such tile
+
+
+@pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
+@pytest.mark.parametrize("first", [False, True])
+@pytest.mark.parametrize("rows,waves", [(2, 4), (2, 8), (4, 4)])
+@pytest.mark.parametrize("case", [0, 2, 3])
+def test_tb2_delta_sweep_matches_reference(C, dtype, first, rows, waves, case):
+    """Increment form: the C level receives d^{m+1}, D receives u^{m+1}; errors of u^m, u^{m+1}."""
+    from wave3d.ops import kernels, reference
+
+    (X, Y, Z), boxes, cdom, chunk = CASES[case]
+    G = 2
+    shape = (X + 2 * G, Y + 2 * G, Z + 2 * G)
+    A = _rand(shape, dtype, 7)
+    Dm1 = (_rand(shape, dtype, 8) - 0.5) * 1e-3  # increments are small
+    tx, ty, tz = _tables(max(shape), dtype, 9)
+    dC = torch.full(shape, -7.0, dtype=dtype, device=DEV)
+    dD = torch.full(shape, -9.0, dtype=dtype, device=DEV)
+    errC, errD = kernels.new_err(1), kernels.new_err(1)
+    ei = (min(b[0] for b in boxes), max(b[1] for b in boxes))
+    kernels.tb_sweep(A.to(DEV), Dm1.to(DEV), dC, dD, boxes, first=first, cdom=cdom, err_i=ei,
+                     tx=tx.to(DEV), ty=ty.to(DEV), tz=tz.to(DEV),
+                     coefs_c=(*COEF.values(), COEFS[0], CT[0]), coefs_d=(*COEF.values(), COEFS[1], CT[1]),
+                     err_c=errC, err_d=errD, rows=rows, waves=waves, chunk=chunk, delta=True)
+    torch.cuda.synchronize()
+    cast = lambda v: torch.tensor(v, dtype=dtype).item()  # noqa: E731
+    h = {k: cast(v) for k, v in COEF.items()}
+    Cf, Df, dn = reference.chained_delta(A, Dm1, first=first, mask=_mask(shape, G, cdom),
+                                         coefs=[cast(COEFS[0]), cast(COEFS[1])], **h)
+    gC, gD = dC.cpu(), dD.cpu()
+    for b in boxes:
+        s = _sl(b, G)
+        _check(gC[s], dn[s], dtype)
+        _check(gD[s], Df[s], dtype)
+    if len(boxes) == 1:
+        s = _sl(boxes[0], G)
+        _check_err(errC, Cf[s], boxes[0], ei, tx, ty, tz, CT[0], dtype)
+        _check_err(errD, gD[s], boxes[0], ei, tx, ty, tz, CT[1], dtype)
