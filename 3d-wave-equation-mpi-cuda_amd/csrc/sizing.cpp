@@ -39,11 +39,11 @@ Layout plan_layout(const Config& c, int world) {
     l.tb = auto_tb || tb3 || c.kernel.rfind("tb2", 0) == 0;
     l.depth = tb3 ? 3 : (l.tb ? 2 : 1);
     if (tb3) l.rows = 2, l.waves = 8;  // measured best three-layer tile (profiles/)
-    // fp32: 16-row tiles (tb2r4, 95 VGPRs) beat 8-row ones by ~4 % at N=512; fp64: 16-row
-    // tiles of 8 waves (tb2r2w8, 128 VGPRs, 2 workgroups per CU) beat 8-row ones by 2-3 %
-    // (profiles/sweep_tb2_vgpr128_r2.txt, profiles/ab_tiles_r2.txt)
-    if (auto_tb && c.dtype == DType::F32) l.rows = 4;
-    if (auto_tb && c.dtype == DType::F64) l.waves = 8;
+    // 16-row tiles of 8 waves (tb2r2w8, 2 workgroups per CU): fp64 +2-3 % over r2w4 (128
+    // VGPRs, 4 waves/SIMD), fp32 +3.5 % (N=512) / +5 % (N=2048) over tb2r4 (profiles/
+    // ab_tiles_r2.txt, fp32_accuracy_r2.txt). The fp64 increment form needs a few more
+    // registers: r2w8 drops to 3 waves/SIMD there, so it keeps the 8-row r2w4 tiles.
+    if (auto_tb && !(c.delta && c.dtype == DType::F64)) l.waves = 8;
     if (l.tb && !auto_tb) parse_tb(c.kernel, l.rows, l.waves, l.occ);
     l.G = l.depth;      // ghost depth = layers per sweep
     l.L = l.depth + 2;  // 3 / 4 / 5 time levels (tb3: C never stored, D and E written)
