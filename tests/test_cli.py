@@ -85,3 +85,25 @@ def test_json_summary(cpu_prog, tmp_path):
     assert d["N"] == 16 and d["timesteps"] == 10 and d["backend"] == "cpu"
     assert d["linf_abs"] > 0 and d["mpts_per_s"] > 0
     assert not os.path.exists(tmp_path / "output_N16_Np2.txt")
+
+
+def test_package_is_an_ordinary_module_tree(C):
+    """`import wave3d` from the checkout yields a normal package (importlib spec, real file,
+    submodules by name), so pickling and introspection work."""
+    import pickle
+
+    import wave3d
+    from wave3d.models import wave
+
+    assert wave3d.__spec__.origin.endswith("3d-wave-equation-mpi-cuda_amd/__init__.py")
+    assert wave.__name__ == "wave3d.models.wave"
+    p = wave3d.WaveProblem(64, timesteps=30, scheme="delta")
+    assert pickle.loads(pickle.dumps(p)) == p
+
+
+def test_console_entry_point_runs_the_cpu_program(C, tmp_path, monkeypatch):
+    from wave3d import cli
+
+    monkeypatch.chdir(tmp_path)
+    assert cli.cpu_main(["16", "2", "pi", "pi", "pi", "1", "10", "--quiet"]) == 0
+    assert (tmp_path / "output_N16_Np2.txt").exists()
