@@ -87,3 +87,17 @@ def test_bench_plan_maps_gpu_counts_to_baseline_configs(C):
     assert (p8["N"], p8["dims"], p8["golden"]) == (1024, [2, 2, 2], 8.04265e-08)
     assert p8["scaling"] == "weak" and p2["scaling"] == "strong"
     assert C.dims_create(4, [0, 0, 0]) == p4["dims"] and C.dims_create(8, [0, 0, 0]) == p8["dims"]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,N,dims", [(2, 512, [2, 1, 1]), (4, 1024, [2, 2, 1]), (8, 1024, [2, 2, 2])])
+def test_bench_gpu_multirank_plan_staged(n, N, dims):
+    """The multi-GPU benchmark path end to end with n processes on one MI355X (staged device
+    transport; RCCL refuses duplicate GPUs): each n runs its BASELINE config and decomposition.
+    Few layers (unstable Courant number, plumbing only), so the L-inf is not checked."""
+    r = _bench(["--steps", "1", "--warmup", "0", "--timesteps", "6", "--transport", "staged",
+                "--shared-device"], nproc=n, timeout=600)
+    assert r["n_gpus"] == n and r["config"]["N"] == N and r["config"]["dims"] == dims
+    assert r["config"]["transport"] == "staged.gloo" and r["rccl_nranks"] is None
+    assert r["config"]["overlap"] is True and r["value"] > 0
+    assert r["timers_ms"]["exchange_ms"] > 0
