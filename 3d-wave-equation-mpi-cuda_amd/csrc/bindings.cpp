@@ -186,7 +186,7 @@ StepCoefs tocoefs(const std::vector<double>& c) {
 
 // One temporal-blocking sweep (k_tb2) on dense tensors: C = u^m, D = u^{m+1} from A, B.
 template <class T>
-void k_tb2_dense(int rows, int waves, bool delta, bool first, uintptr_t A, uintptr_t B, uintptr_t Cc, uintptr_t D,
+void k_tb2_dense(int rows, int waves, int nwk, bool delta, bool first, uintptr_t A, uintptr_t B, uintptr_t Cc, uintptr_t D,
                  const std::vector<i64>& g, const std::vector<std::vector<int>>& boxes,
                  const std::vector<int>& cdom, int ei0, int ei1, const std::vector<int>& wrapC,
                  const std::vector<int>& wrapD, uintptr_t tx, uintptr_t ty, uintptr_t tz,
@@ -197,7 +197,7 @@ void k_tb2_dense(int rows, int waves, bool delta, bool first, uintptr_t A, uintp
     W3D_REQUIRE(v.G >= 2, "k_tb2 needs ghost depth >= 2");
     std::vector<Box> bx;
     for (auto& b : boxes) bx.push_back(tobox(b));
-    launch_tb2<T>(rows, waves, 0, delta, first, P<T>(A) + o, P<T>(B) + o, P<T>(Cc) + o, P<T>(D) + o, v,
+    launch_tb2<T>(rows, waves, 0, nwk, delta, first, P<T>(A) + o, P<T>(B) + o, P<T>(Cc) + o, P<T>(D) + o, v,
                   bx.data(), int(bx.size()), tobox(cdom), ei0, ei1, towrap(wrapC), towrap(wrapD),
                   SeamAlias<T>{}, P<T>(tx), P<T>(ty), P<T>(tz), tocoefs(cC), tocoefs(cD),
                   P<u64>(errC), P<u64>(errD), chunk, (hipStream_t)stream);
@@ -393,9 +393,9 @@ PYBIND11_MODULE(_wave3d_C, m) {
     m.def("k_tb2_f32", &k_tb2_dense<float>);
     m.def("k_tb3_f64", &k_tb3_dense<double>);
     m.def("k_tb3_f32", &k_tb3_dense<float>);
-    m.def("tb_supported", [](int depth, int rows, int waves) {
-        return depth == 3 ? tb3_supported(rows, waves) : tb2_supported(rows, waves, 0);
-    });
+    m.def("tb_supported", [](int depth, int rows, int waves, int nwk) {
+        return depth == 3 ? tb3_supported(rows, waves) : tb2_supported(rows, waves, 0, nwk);
+    }, py::arg("depth"), py::arg("rows"), py::arg("waves"), py::arg("nwk") = 1);
     m.def("k_init_f64", &k_init<double>);
     m.def("k_init_f32", &k_init<float>);
     m.def("k_faces_f64", &k_faces<double>);

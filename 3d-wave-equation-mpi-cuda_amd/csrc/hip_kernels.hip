@@ -477,6 +477,14 @@ __global__ void __launch_bounds__(kThreads) k_box_copy(const BoxCopyOps<T> ops, 
 
 int march_rows_per_thread() { return 4; }
 
+bool tile_order_jfirst() {
+    static const bool on = [] {
+        const char* e = std::getenv("WAVE3D_TILE_ORDER");
+        return !(e && e[0] == 'k');
+    }();
+    return on;
+}
+
 bool xcd_swizzle_enabled() {
     static const bool on = [] {
         const char* e = std::getenv("WAVE3D_XCD_SWIZZLE");

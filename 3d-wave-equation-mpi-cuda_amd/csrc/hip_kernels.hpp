@@ -155,6 +155,11 @@ int march_rows_per_thread();
 // XCD-aware workgroup order for the stencil kernels (device_common.hpp xcd_swizzle);
 // opt-in via env WAVE3D_XCD_SWIZZLE=1 (ablation, not faster on MI355X).
 bool xcd_swizzle_enabled();
+// Temporal-blocking tile order: j-neighbour tiles at consecutive block ids, so k-neighbours are
+// a multiple of 8 ids apart and share an XCD (their halo lines then hit that XCD's L2: -17 %
+// memory-side reads, profiles/tile_order_r2.txt). Default; WAVE3D_TILE_ORDER=k restores the
+// k-fastest order (A/B switch).
+bool tile_order_jfirst();
 
 // Temporal blocking: one sweep computes layers m (C) and m+1 (D) from A = u^{m-1} and
 // B = u^{m-2} (unused when m == 1), D-boxes as for launch_step. C is evaluated on a one-node
@@ -171,14 +176,15 @@ struct SeamAlias {
     const T* prev = nullptr;
 };
 
-// `rows` per lane x `waves` wave64s per workgroup = tile height (tb2_supported()).
-// `occ` > 0 caps registers so that many waves fit per SIMD (may spill a little).
-bool tb2_supported(int rows, int waves, int occ = 0);
+// Tile = (waves / nwk) * rows rows x 64 * nwk columns (nwk waves side by side along k);
+// tb2_supported() lists the instantiated shapes. `occ` > 0 caps registers so that many waves
+// fit per SIMD (may spill a little).
+bool tb2_supported(int rows, int waves, int occ = 0, int nwk = 1);
 // delta: increment form — B holds d^{m-1}; C receives d^{m+1} (planes of D, with C's wrap
 // planes), D receives u^{m+1}; u^m is formed in registers for its errors only.
-bool tb2_delta_supported(int rows, int waves);
+bool tb2_delta_supported(int rows, int waves, int nwk = 1);
 template <class T>
-void launch_tb2(int rows, int waves, int occ, bool delta, bool first, const T* A, const T* B, T* C, T* D, const GridView& gv,
+void launch_tb2(int rows, int waves, int occ, int nwk, bool delta, bool first, const T* A, const T* B, T* C, T* D, const GridView& gv,
                 const Box* boxes, int nbox, const Box& cdom, int ei0, int ei1, const Wrap& wrapC,
                 const Wrap& wrapD, const SeamAlias<T>& alias, const T* tx, const T* ty,
                 const T* tz, const StepCoefs& cC, const StepCoefs& cD, u64* errC, u64* errD,

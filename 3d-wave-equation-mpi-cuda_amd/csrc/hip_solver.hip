@@ -41,11 +41,12 @@ namespace {
 using clk = std::chrono::steady_clock;
 
 // Temporal-blocking variant names: "tb2" (2 rows/lane, 4 waves), "tb2r<R>", "tb2r<R>w<W>".
-std::string tb_name(int rows, int waves, int occ, int depth = 2) {
+std::string tb_name(int rows, int waves, int occ, int depth = 2, int kwaves = 1) {
     if (depth == 3)
         return rows == 2 && waves == 8 ? "tb3" : "tb3r" + std::to_string(rows) + "w" + std::to_string(waves);
-    std::string s = rows == 2 && waves == 4 && occ == 0 ? "tb2" : "tb2r" + std::to_string(rows);
-    if (waves != 4 || occ) s += "w" + std::to_string(waves);
+    std::string s = rows == 2 && waves == 4 && occ == 0 && kwaves == 1 ? "tb2" : "tb2r" + std::to_string(rows);
+    if (waves != 4 || occ || kwaves != 1) s += "w" + std::to_string(waves);
+    if (kwaves != 1) s += "k" + std::to_string(kwaves);
     if (occ) s += "o" + std::to_string(occ);
     return s;
 }
@@ -123,11 +124,12 @@ public:
         tb_rows_ = lay.rows;
         tb_waves_ = lay.waves;
         tb_occ_ = lay.occ;
+        tb_nwk_ = lay.kwaves;
         G_ = lay.G;
         L_ = lay.L;
         for (int a = 0; a < 3; ++a) cfg_.dims[a] = lay.dims[a];
         W3D_REQUIRE(!tb_ || (tbd_ == 3 ? tb3_supported(tb_rows_, tb_waves_)
-                                        : tb2_supported(tb_rows_, tb_waves_, tb_occ_)),
+                                        : tb2_supported(tb_rows_, tb_waves_, tb_occ_, tb_nwk_)),
                     "wave3d: unknown kernel variant " + c.kernel);
         kind_ = parse_kernel_variant(tb_ ? std::string("auto") : c.kernel);
         naive_.march = false;
@@ -176,7 +178,7 @@ public:
         if (log_on(LogLevel::Info)) {
             for (auto& R : ranks_) {
                 log_msg(LogLevel::Info, R.topo.describe(), " kernel ",
-                        tb_ ? tb_name(tb_rows_, tb_waves_, tb_occ_, tbd_) : kernel_variant_name(kind_), " levels ",
+                        tb_ ? tb_name(tb_rows_, tb_waves_, tb_occ_, tbd_, tb_nwk_) : kernel_variant_name(kind_), " levels ",
                         L_, " ghost ", G_, " bytes/level ", R.elems * sizeof(T), " overlap ",
                         overlap_ ? "on" : "off", " transport ",
                         ext_ ? ext_->name() : (world_ > 1 ? "loopback" : "self"));
@@ -199,7 +201,7 @@ public:
         res.Np = world_;
         res.dtype = cfg_.dtype;
         res.backend = "hip";
-        res.kernel = tb_ ? tb_name(tb_rows_, tb_waves_, tb_occ_, tbd_) : kernel_variant_name(kind_);
+        res.kernel = tb_ ? tb_name(tb_rows_, tb_waves_, tb_occ_, tbd_, tb_nwk_) : kernel_variant_name(kind_);
         res.courant = prob_.courant;
         res.transport = ext_ ? ext_->name() : (world_ > 1 ? "loopback" : "self");
         res.overlap = overlap_;
@@ -571,7 +573,7 @@ private:
         // and last x-ranks send one plane deeper, skipping the periodic duplicate plane), so the
         // exchange can start as soon as the shells are done, while the interior still runs.
         Box c = R.compute, in = c;
-        const int TJ = tb_rows_ * tb_waves_;
+        const int TJ = tb_rows_ * tb_waves_ / tb_nwk_, TKs = kTileK * tb_nwk_;
         if (!R.plan.self_x) {
             const int xs = t.dims[0] > 1 ? 1 : 0;  // one x rank messaging itself: both ends
             in.i0 = std::max(in.i0, 1 + dA + ((t.first(0) || !xs) ? 1 : 0));
@@ -579,8 +581,8 @@ private:
         }
         if (t.nbr[1][0] >= 0) in.j0 = std::max(in.j0, std::max(1 + dA, c.j0 + TJ));
         if (t.nbr[1][1] >= 0) in.j1 = std::min(in.j1, std::min(Y - dA, c.j1 - TJ));
-        if (t.nbr[2][0] >= 0) in.k0 = std::max(in.k0, 1 + kTileK * ((dA + kTileK - 1) / kTileK));
-        if (t.nbr[2][1] >= 0) in.k1 = std::min(in.k1, kTileK * ((Z - dA) / kTileK));
+        if (t.nbr[2][0] >= 0) in.k0 = std::max(in.k0, 1 + TKs * ((dA + TKs - 1) / TKs));
+        if (t.nbr[2][1] >= 0) in.k1 = std::min(in.k1, TKs * ((Z - dA) / TKs));
         R.tb_interior = in;
         auto add = [&](Box b) {
             if (!b.empty()) R.tb_shell.push_back(b);
@@ -707,7 +709,7 @@ private:
             al.prev = R.alias_buf + R.plane_off;
         }
         if (!boxes) boxes = &R.compute, nbox = 1;
-        launch_tb2<T>(tb_rows_, tb_waves_, tb_occ_, cfg_.delta, m == 1, A, B, R.g[lvl(m)], R.g[lvl(m + 1)], R.gv, boxes, nbox,
+        launch_tb2<T>(tb_rows_, tb_waves_, tb_occ_, tb_nwk_, cfg_.delta, m == 1, A, B, R.g[lvl(m)], R.g[lvl(m + 1)], R.gv, boxes, nbox,
                       R.cdom, R.error.i0, R.error.i1, R.wrap, R.wrap2, al, R.tx, R.ty, R.tz,
                       coefs(m), coefs(m + 1), R.err + size_t(m) * kSlotsPerLayer,
                       R.err + size_t(m + 1) * kSlotsPerLayer, cfg_.chunk, s);
@@ -1310,6 +1312,7 @@ private:
     int tb_rows_ = 2;
     int tb_waves_ = 4;
     int tb_occ_ = 0;
+    int tb_nwk_ = 1;    // tb2 waves along k (tile width 64 * tb_nwk_)
     int tbd_ = 1;       // layers per sweep (1, 2 or 3)
     hipGraphExec_t gexec_ = nullptr;  // captured IC + time loop (graph_eligible())
     bool graph_failed_ = false;

@@ -33,7 +33,8 @@ namespace {
 
 template <class T>
 struct TbParams {
-    int xcd;  // XCD-aware tile order (xcd_swizzle)
+    int xcd;     // XCD-aware tile order (xcd_swizzle)
+    int jfirst;  // tile order: j-neighbours at consecutive block ids (k-neighbours share an XCD)
     const T* A;
     const T* B;
     T* C;
@@ -76,14 +77,23 @@ struct TbParams {
 // DELTA: increment form (csrc/hip_kernels.hpp launch_tb2): B = d^{m-1}; d^m = B + coefC*lap A,
 // C = A + d^m (registers: errors, D's stencil); d^{m+1} = d^m + coefD*lap C, D = C + d^{m+1};
 // the C level receives d^{m+1} at D's planes, so the store count is unchanged.
-template <class T, bool FIRST, int R, int NW, int WPE = 1, int ABL = 0, int OPT = 0, bool DELTA = false>
+// NWK: waves side by side along k — the tile is (NW/NWK)*R rows x 64*NWK columns. Wider tiles
+// halve the k-side halo lines per own line (each row's halo columns kb-2..kb-1 and
+// kb+TK..kb+TK+1 sit in two 128-B lines owned by the k-neighbour tile, which runs on another
+// XCD, so they are fetched again from beyond L2 — the bulk of tb2's read surplus,
+// profiles/dram_bytes_r2.txt).
+template <class T, bool FIRST, int R, int NW, int WPE = 1, int ABL = 0, int OPT = 0, bool DELTA = false,
+          int NWK = 1>
 __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WPE, 8))) k_tb2(const TbParams<T> p) {
-    constexpr int TJ = NW * R;
-    constexpr int AH = TJ + 4, AW = kTK + 4;  // A tile: rows jt-2..jt+TJ+1, cols kb-2..kb+65
-    constexpr int CH = TJ + 2, CW = kTK + 2;  // C tile: rows jt-1..jt+TJ,   cols kb-1..kb+64
+    static_assert(NW % NWK == 0, "waves along k must divide the workgroup");
+    constexpr int NWJ = NW / NWK;
+    constexpr int TK = kTK * NWK;             // tile columns
+    constexpr int TJ = NWJ * R;               // tile rows
+    constexpr int AH = TJ + 4, AW = TK + 4;   // A tile: rows jt-2..jt+TJ+1, cols kb-2..kb+TK+1
+    constexpr int CH = TJ + 2, CW = TK + 2;   // C tile: rows jt-1..jt+TJ,   cols kb-1..kb+TK
     constexpr unsigned ES = sizeof(T);
     constexpr int kStAux = (OPT & 1) ? 0 : 2;  // store cache policy: 2 = non-temporal
-    static_assert(128 + 2 * CH <= NW * 64 && 132 + 2 * CH <= NW * 64, "ring needs more lanes");
+    static_assert(2 * TK + 2 * CH <= NW * 64 && 2 * (TK + 2) + 2 * CH <= NW * 64, "ring needs more lanes");
     __shared__ T ldsA[2][AH][AW];
     __shared__ T ldsC[2][CH][CW];
 
@@ -91,16 +101,27 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WP
     const int b = find_box(p, bid);
     const BoxLaunch Bx = p.box[b];
     int local = bid - Bx.block_begin;
-    const int tk = local % Bx.tiles_k;
-    local /= Bx.tiles_k;
-    const int tj = local % Bx.tiles_j;
-    const int ci = local / Bx.tiles_j;
-    const int kb = Bx.kbase + tk * kTK;
+    int tk, tj;
+    if (p.jfirst) {
+        tj = local % Bx.tiles_j;
+        local /= Bx.tiles_j;
+        tk = local % Bx.tiles_k;
+        local /= Bx.tiles_k;
+    } else {
+        tk = local % Bx.tiles_k;
+        local /= Bx.tiles_k;
+        tj = local % Bx.tiles_j;
+        local /= Bx.tiles_j;
+    }
+    const int ci = local;
+    const int kb = Bx.kbase + tk * TK;
     const int jt = Bx.j0 + tj * TJ;
     const int ib = Bx.i0 + ci * Bx.chunk;
     const int ie = min(Bx.i1, ib + Bx.chunk - 1);
     const int lane = threadIdx.x & 63;
-    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int w8 = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int w = w8 % NWJ;                 // wave's row band
+    const int kl = (w8 / NWJ) * kTK + lane;  // column within the tile
     const i64 si = p.si;
     const int sj = p.sj;
     const unsigned pbytes = unsigned(si) * ES;
@@ -113,7 +134,7 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WP
     auto prs = [&](const T* base, int i) { return plane_rsrc(base + (i64(i) * si - p.poff), pbytes); };
 
     // ---- own nodes (D and C) ----------------------------------------------------------
-    const int k = kb + lane;
+    const int k = kb + kl;
     unsigned oa[R], ob[R], os[R];  // A-load, B-load, store offsets (kOOB when masked)
     bool ovalid[R], ocd[R];
     T oty[R];
@@ -130,15 +151,15 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WP
     const T otz = (k >= Bx.k0 && k <= Bx.k1) ? p.tz[k] : T(0);
 
     // ---- C-ring node of this thread (rolling A, C into the LDS tile only) --------------
-    // rows jt-1 / jt+TJ over cols kb..kb+63, then cols kb-1 / kb+64 over rows jt-1..jt+TJ
+    // rows jt-1 / jt+TJ over cols kb..kb+TK-1, then cols kb-1 / kb+TK over rows jt-1..jt+TJ
     int rj = 0, rk = 0;
     bool ron = false;
     {
         const int q = threadIdx.x;
-        if (q < 64) rj = jt - 1, rk = kb + q, ron = true;
-        else if (q < 128) rj = jt + TJ, rk = kb + q - 64, ron = true;
-        else if (q < 128 + CH) rj = jt - 1 + (q - 128), rk = kb - 1, ron = true;
-        else if (q < 128 + 2 * CH) rj = jt - 1 + (q - 128 - CH), rk = kb + kTK, ron = true;
+        if (q < TK) rj = jt - 1, rk = kb + q, ron = true;
+        else if (q < 2 * TK) rj = jt + TJ, rk = kb + q - TK, ron = true;
+        else if (q < 2 * TK + CH) rj = jt - 1 + (q - 2 * TK), rk = kb - 1, ron = true;
+        else if (q < 2 * TK + 2 * CH) rj = jt - 1 + (q - 2 * TK - CH), rk = kb + TK, ron = true;
     }
     const bool rcd = ron && incd(rj, rk);
     const unsigned ra_off = boff(rj, rk, ron && inb(rj, rk));
@@ -149,10 +170,11 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WP
     bool uon = false;
     {
         const int q = threadIdx.x;
-        if (q < 66) uj = jt - 2, uk = kb - 1 + q, uon = true;
-        else if (q < 132) uj = jt + TJ + 1, uk = kb - 1 + (q - 66), uon = true;
-        else if (q < 132 + CH) uj = jt - 1 + (q - 132), uk = kb - 2, uon = true;
-        else if (q < 132 + 2 * CH) uj = jt - 1 + (q - 132 - CH), uk = kb + kTK + 1, uon = true;
+        constexpr int RW = TK + 2;  // outer ring rows jt-2 / jt+TJ+1: cols kb-1..kb+TK
+        if (q < RW) uj = jt - 2, uk = kb - 1 + q, uon = true;
+        else if (q < 2 * RW) uj = jt + TJ + 1, uk = kb - 1 + (q - RW), uon = true;
+        else if (q < 2 * RW + CH) uj = jt - 1 + (q - 2 * RW), uk = kb - 2, uon = true;
+        else if (q < 2 * RW + 2 * CH) uj = jt - 1 + (q - 2 * RW - CH), uk = kb + TK + 1, uon = true;
     }
     const unsigned ua_off = boff(uj, uk, uon && inb(uj, uk));
 
@@ -219,7 +241,7 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WP
         constexpr int P = decltype(phase)::value;
         constexpr int S1 = (P + 1) & 3, H0 = P & 1;
 #pragma unroll
-        for (int r = 0; r < R; ++r) ldsA[H0][2 + w * R + r][2 + lane] = a[S1][r];
+        for (int r = 0; r < R; ++r) ldsA[H0][2 + w * R + r][2 + kl] = a[S1][r];
         if (ron) ldsA[H0][rj - jt + 2][rk - kb + 2] = ra[S1];
         if (uon) ldsA[H0][uj - jt + 2][uk - kb + 2] = ua[S1];
     };
@@ -251,7 +273,7 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WP
         // C(i) on own nodes and the ring (0 on Dirichlet faces)
 #pragma unroll
         for (int r = 0; r < R; ++r) {
-            const int ya = 2 + w * R + r, xa = 2 + lane;
+            const int ya = 2 + w * R + r, xa = 2 + kl;
             const T lap = laplace7_cr(a[S1][r], xpA[r], xnA[r], ldsA[H0][ya - 1][xa],
                                       ldsA[H0][ya + 1][xa], ldsA[H0][ya][xa - 1],
                                       ldsA[H0][ya][xa + 1], p.hx2, p.hy2, p.hz2, p.yx2, p.yy2,
@@ -266,7 +288,7 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WP
                            : leapfrog(a[S1][r], bb[H0][r], lap, p.coefC);
             }
             c[S0][r] = ocd[r] ? cv : T(0);
-            ldsC[H0][1 + w * R + r][1 + lane] = c[S0][r];
+            ldsC[H0][1 + w * R + r][1 + kl] = c[S0][r];
         }
         if (ron) {
             const int ya = rj - jt + 2, xa = rk - kb + 2;
@@ -314,7 +336,7 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WP
             T dv[R];
 #pragma unroll
             for (int r = 0; r < R; ++r) {
-                const int yc = 1 + w * R + r, xc = 1 + lane;
+                const int yc = 1 + w * R + r, xc = 1 + kl;
                 const T lap = laplace7_cr(c[S3][r], c[S2][r], c[S0][r], ldsC[H1][yc - 1][xc],
                                           ldsC[H1][yc + 1][xc], ldsC[H1][yc][xc - 1],
                                           ldsC[H1][yc][xc + 1], p.hx2, p.hy2, p.hz2, p.yx2,
@@ -393,21 +415,29 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WP
 
 // increment form: the main tile shapes only
 template <class T, bool F>
-static void (*tb_delta_kernel(int rows, int waves))(const TbParams<T>) {
-    switch (rows * 10 + waves) {
-        case 24: return k_tb2<T, F, 2, 4, 1, 0, 0, true>;
-        case 28: return k_tb2<T, F, 2, 8, 1, 0, 0, true>;
-        case 44: return k_tb2<T, F, 4, 4, 1, 0, 0, true>;
+static void (*tb_delta_kernel(int rows, int waves, int nwk))(const TbParams<T>) {
+    switch (rows * 100 + waves * 10 + nwk) {
+        case 241: return k_tb2<T, F, 2, 4, 1, 0, 0, true>;
+        case 281: return k_tb2<T, F, 2, 8, 1, 0, 0, true>;
+        case 441: return k_tb2<T, F, 4, 4, 1, 0, 0, true>;
+        case 282: return k_tb2<T, F, 2, 8, 1, 0, 0, true, 2>;
         default: return nullptr;
     }
 }
 
-bool tb2_delta_supported(int rows, int waves) { return tb_delta_kernel<double, false>(rows, waves) != nullptr; }
+bool tb2_delta_supported(int rows, int waves, int nwk) {
+    return tb_delta_kernel<double, false>(rows, waves, nwk) != nullptr;
+}
 
 // rows x waves (x minimum waves per SIMD: register cap for the compiler, 0 = none)
 template <class T, bool F>
-static void (*tb_kernel(int rows, int waves, int occ))(const TbParams<T>) {
-    switch (rows * 1000 + waves * 10 + occ) {
+static void (*tb_kernel(int rows, int waves, int occ, int nwk))(const TbParams<T>) {
+    switch (rows * 1000 + waves * 10 + occ + (nwk - 1) * 100000) {
+        // 128-column tiles (two waves side by side along k)
+        case 102080: return k_tb2<T, F, 2, 8, 1, 0, 0, false, 2>;
+        case 102084: return k_tb2<T, F, 2, 8, 4, 0, 0, false, 2>;
+        case 104080: return k_tb2<T, F, 4, 8, 1, 0, 0, false, 2>;
+        case 102160: return k_tb2<T, F, 2, 16, 1, 0, 0, false, 2>;
         case 2040: {
             static const int abl = [] {
                 const char* e = std::getenv("WAVE3D_TB_ABLATION");
@@ -434,23 +464,24 @@ static void (*tb_kernel(int rows, int waves, int occ))(const TbParams<T>) {
     }
 }
 
-bool tb2_supported(int rows, int waves, int occ) {
-    return tb_kernel<double, false>(rows, waves, occ) != nullptr;
+bool tb2_supported(int rows, int waves, int occ, int nwk) {
+    return tb_kernel<double, false>(rows, waves, occ, nwk) != nullptr;
 }
 
 template <class T>
-void launch_tb2(int rows, int waves, int occ, bool delta, bool first, const T* A, const T* B, T* C, T* D, const GridView& gv,
+void launch_tb2(int rows, int waves, int occ, int nwk, bool delta, bool first, const T* A, const T* B, T* C, T* D, const GridView& gv,
                 const Box* boxes, int nbox, const Box& cdom, int ei0, int ei1, const Wrap& wrapC,
                 const Wrap& wrapD, const SeamAlias<T>& alias, const T* tx, const T* ty,
                 const T* tz, const StepCoefs& cC, const StepCoefs& cD, u64* errC, u64* errD,
                 int chunk, hipStream_t s) {
     W3D_REQUIRE(gv.G >= 2, "temporal blocking needs ghost depth >= 2");
-    W3D_REQUIRE(tb2_supported(rows, waves, occ), "tb2: unsupported rows x waves x occupancy");
-    W3D_REQUIRE(!delta || (occ == 0 && tb2_delta_supported(rows, waves)),
-                "tb2 increment form: tiles r2w4, r2w8, r4w4 only");
+    W3D_REQUIRE(tb2_supported(rows, waves, occ, nwk), "tb2: unsupported rows x waves x occupancy x k-waves");
+    W3D_REQUIRE(!delta || (occ == 0 && tb2_delta_supported(rows, waves, nwk)),
+                "tb2 increment form: tiles r2w4, r2w8, r4w4, r2w8k2 only");
     W3D_REQUIRE(nbox >= 1 && nbox <= kMaxBoxes, "bad box count");
     TbParams<T> p{};
     p.xcd = xcd_swizzle_enabled();
+    p.jfirst = tile_order_jfirst();
     p.A = A;
     p.B = B;
     p.C = C;
@@ -489,7 +520,7 @@ void launch_tb2(int rows, int waves, int occ, bool delta, bool first, const T* A
     p.ctD = T(cD.ct);
     p.errC = errC;
     p.errD = errD;
-    const int TJ = waves * rows;
+    const int TJ = waves / nwk * rows, TK = kTK * nwk;
     int nb = 0, total = 0;
     for (int q = 0; q < nbox; ++q) {
         const Box& bx = boxes[q];
@@ -499,13 +530,13 @@ void launch_tb2(int rows, int waves, int occ, bool delta, bool first, const T* A
                     "sweep box outside the owned region");
         BoxLaunch& L = p.box[nb];
         L.i0 = bx.i0, L.i1 = bx.i1, L.j0 = bx.j0, L.j1 = bx.j1, L.k0 = bx.k0, L.k1 = bx.k1;
-        const int t0 = (bx.k0 - 1) / kTK, t1 = (bx.k1 - 1) / kTK;
-        L.kbase = 1 + t0 * kTK;
+        const int t0 = (bx.k0 - 1) / TK, t1 = (bx.k1 - 1) / TK;
+        L.kbase = 1 + t0 * TK;
         L.tiles_k = t1 - t0 + 1;
         L.tiles_j = cdiv(bx.j1 - bx.j0 + 1, TJ);
         const int planes = bx.i1 - bx.i0 + 1;
         const int want = chunk > 0 ? std::min(chunk, planes)
-                                   : auto_chunk(96, planes, L.tiles_k * L.tiles_j);
+                                   : auto_chunk(96, planes, L.tiles_k * L.tiles_j * nwk);
         L.chunk = cdiv(planes, cdiv(planes, want));  // equal work items (no short tail chunk)
         L.block_begin = total;
         total += L.tiles_k * L.tiles_j * cdiv(planes, L.chunk);
@@ -513,14 +544,14 @@ void launch_tb2(int rows, int waves, int occ, bool delta, bool first, const T* A
     }
     p.nbox = nb;
     if (nb == 0) return;
-    auto kern = delta ? (first ? tb_delta_kernel<T, true>(rows, waves) : tb_delta_kernel<T, false>(rows, waves))
-                      : (first ? tb_kernel<T, true>(rows, waves, occ) : tb_kernel<T, false>(rows, waves, occ));
+    auto kern = delta ? (first ? tb_delta_kernel<T, true>(rows, waves, nwk) : tb_delta_kernel<T, false>(rows, waves, nwk))
+                      : (first ? tb_kernel<T, true>(rows, waves, occ, nwk) : tb_kernel<T, false>(rows, waves, occ, nwk));
     hipLaunchKernelGGL(kern, dim3(total), dim3(waves * 64), 0, s, p);
     HIP_OK(hipGetLastError());
 }
 
 #define W3D_TB_INST(T)                                                                       \
-    template void launch_tb2<T>(int, int, int, bool, bool, const T*, const T*, T*, T*, const GridView&, \
+    template void launch_tb2<T>(int, int, int, int, bool, bool, const T*, const T*, T*, T*, const GridView&, \
                                 const Box*, int, const Box&, int, int, const Wrap&,          \
                                 const Wrap&, const SeamAlias<T>&, const T*, const T*,        \
                                 const T*, const StepCoefs&, const StepCoefs&, u64*, u64*,    \

@@ -7,25 +7,23 @@
 
 namespace wave3d {
 
-static void parse_tb(const std::string& name, int& rows, int& waves, int& occ) {
+// "tb2[r<R>][w<W>][k<NWK>][o<OCC>]" / "tb3[r<R>w<W>]"
+static void parse_tb(const std::string& name, int& rows, int& waves, int& occ, int& kwaves) {
     if (name.rfind("tb3", 0) != 0) rows = 2, waves = 4;
     occ = 0;
+    kwaves = 1;
     std::string s = name.substr(3);
-    if (!s.empty() && s[0] == 'r') {
-        size_t n = 0;
-        rows = std::stoi(s.substr(1), &n);
-        s = s.substr(1 + n);
-    }
-    if (!s.empty() && s[0] == 'w') {
-        size_t n = 0;
-        waves = std::stoi(s.substr(1), &n);
-        s = s.substr(1 + n);
-    }
-    if (!s.empty() && s[0] == 'o') {
-        size_t n = 0;
-        occ = std::stoi(s.substr(1), &n);
-        s = s.substr(1 + n);
-    }
+    auto num = [&](char tag, int& out) {
+        if (!s.empty() && s[0] == tag) {
+            size_t n = 0;
+            out = std::stoi(s.substr(1), &n);
+            s = s.substr(1 + n);
+        }
+    };
+    num('r', rows);
+    num('w', waves);
+    num('k', kwaves);
+    num('o', occ);
     W3D_REQUIRE(s.empty(), "wave3d: unknown kernel variant " + name);
 }
 
@@ -44,7 +42,7 @@ Layout plan_layout(const Config& c, int world) {
     // ab_tiles_r2.txt, fp32_accuracy_r2.txt). The fp64 increment form needs a few more
     // registers: r2w8 drops to 3 waves/SIMD there, so it keeps the 8-row r2w4 tiles.
     if (auto_tb && !(c.delta && c.dtype == DType::F64)) l.waves = 8;
-    if (l.tb && !auto_tb) parse_tb(c.kernel, l.rows, l.waves, l.occ);
+    if (l.tb && !auto_tb) parse_tb(c.kernel, l.rows, l.waves, l.occ, l.kwaves);
     l.G = l.depth;      // ghost depth = layers per sweep
     l.L = l.depth + 2;  // 3 / 4 / 5 time levels (tb3: C never stored, D and E written)
     for (int a = 0; a < 3; ++a) l.dims[a] = c.dims[a];

@@ -15,6 +15,7 @@ struct Layout {
     int depth = 1;            // layers per sweep: 1 (single step), 2 (tb2) or 3 (tb3)
     int rows = 2, waves = 4;  // TB tile shape
     int occ = 0;              // TB register cap (min waves per SIMD, 0 = compiler's choice)
+    int kwaves = 1;           // TB waves side by side along k (tile width 64 * kwaves)
     int G = 1;                // ghost depth
     int L = 3;                // time levels
     int dims[3] = {0, 0, 0};  // decomposition override (0 = Dims_create)

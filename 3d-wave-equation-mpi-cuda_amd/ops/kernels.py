@@ -175,20 +175,21 @@ def _check_box_g(box, gv) -> list[int]:
 
 def tb_sweep(A, B, C, D, boxes, *, first: bool, cdom, err_i, tx, ty, tz, coefs_c, coefs_d,
              err_c, err_d, rows: int = 2, waves: int = 4, chunk: int = 0, wrap_c=None,
-             wrap_d=None, ghost: int = 2, delta: bool = False) -> None:
+             wrap_d=None, ghost: int = 2, delta: bool = False, kwaves: int = 1) -> None:
     """One temporal-blocking sweep (k_tb2): C = u^m and D = u^{m+1} on ``boxes`` from
     A = u^{m-1}, B = u^{m-2} (dense grids with ``ghost`` >= 2 layers; logical indices).
     ``cdom`` = (i0, i1, j0, j1, k0, k1): C is a stencil value inside it in j/k, 0 outside
     (Dirichlet faces); coefs = (hx2, hy2, hz2, coef, ct) per layer. ``delta``: increment form,
-    B holds d^{m-1}, C receives d^{m+1} and D u^{m+1} (u^m only enters the errors)."""
+    B holds d^{m-1}, C receives d^{m+1} and D u^{m+1} (u^m only enters the errors).
+    Tile = (waves / kwaves) * rows rows x 64 * kwaves columns."""
     gv = _check_grid_g(ghost, A, B, C, D)
     if ghost < 2:
         raise ValueError("k_tb2 needs ghost depth >= 2")
     if isinstance(boxes[0], int):
         boxes = [boxes]
     bl = [_check_box_g(b, gv) for b in boxes]
-    if not _C().tb_supported(2, rows, waves):
-        raise ValueError(f"unsupported tile rows={rows} waves={waves}")
+    if not _C().tb_supported(2, rows, waves, kwaves):
+        raise ValueError(f"unsupported tile rows={rows} waves={waves} kwaves={kwaves}")
     for t in (tx, ty, tz):
         if not t.is_cuda or t.dtype != A.dtype or t.numel() < max(gv[:3]):
             raise ValueError("analytic tables must be device tensors covering the grid")
@@ -196,7 +197,7 @@ def tb_sweep(A, B, C, D, boxes, *, first: bool, cdom, err_i, tx, ty, tz, coefs_c
         if e.dtype != torch.int64 or e.numel() < 3 or not e.is_cuda:
             raise ValueError("error slots must be >= 3 int64 device values (new_err())")
     fn = getattr(_C(), "k_tb2_" + _sfx(A))
-    fn(int(rows), int(waves), bool(delta), bool(first), A.data_ptr(), B.data_ptr(), C.data_ptr(),
+    fn(int(rows), int(waves), int(kwaves), bool(delta), bool(first), A.data_ptr(), B.data_ptr(), C.data_ptr(),
        D.data_ptr(), gv, bl, [int(v) for v in cdom], int(err_i[0]), int(err_i[1]), list(wrap_c or []),
        list(wrap_d or []), tx.data_ptr(), ty.data_ptr(), tz.data_ptr(),
        [float(c) for c in coefs_c], [float(c) for c in coefs_d], err_c.data_ptr(),

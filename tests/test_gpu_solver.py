@@ -21,7 +21,7 @@ def _fmt(r):
     return [(fmt6(a), fmt6(b)) for a, b in zip(r.max_abs, r.max_rel)]
 
 
-@pytest.mark.parametrize("kernel", ["march", "naive", "flat", "auto", "march8", "tb2", "tb2r4", "tb2r4w8", "tb2r2w16", "tb3"])
+@pytest.mark.parametrize("kernel", ["march", "naive", "flat", "auto", "march8", "tb2", "tb2r4", "tb2r4w8", "tb2r2w16", "tb3", "tb2r2w8k2", "tb2r2w16k2"])
 def test_golden_n32(C, kernel):
     import wave3d
     from wave3d.utils import GOLDEN_N32_K20

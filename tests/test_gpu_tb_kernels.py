@@ -77,9 +77,9 @@ CASES = [
 
 @pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
 @pytest.mark.parametrize("first", [False, True])
-@pytest.mark.parametrize("rows,waves", [(2, 4), (2, 8), (4, 4)])
+@pytest.mark.parametrize("rows,waves,kw", [(2, 4, 1), (2, 8, 1), (4, 4, 1), (2, 8, 2), (2, 16, 2)])
 @pytest.mark.parametrize("case", range(len(CASES)))
-def test_tb2_sweep_matches_reference(C, dtype, first, rows, waves, case):
+def test_tb2_sweep_matches_reference(C, dtype, first, rows, waves, kw, case):
     from wave3d.ops import kernels, reference
 
     (X, Y, Z), boxes, cdom, chunk = CASES[case]
@@ -96,7 +96,7 @@ def test_tb2_sweep_matches_reference(C, dtype, first, rows, waves, case):
     kernels.tb_sweep(dA, dB, dC, dD, boxes, first=first, cdom=cdom, err_i=ei, tx=tx.to(DEV),
                      ty=ty.to(DEV), tz=tz.to(DEV), coefs_c=(*COEF.values(), COEFS[0], CT[0]),
                      coefs_d=(*COEF.values(), COEFS[1], CT[1]), err_c=errC, err_d=errD,
-                     rows=rows, waves=waves, chunk=chunk)
+                     rows=rows, waves=waves, chunk=chunk, kwaves=kw)
     torch.cuda.synchronize()
     cast = lambda v: torch.tensor(v, dtype=dtype).item()  # noqa: E731
     h = {k: cast(v) for k, v in COEF.items()}
@@ -169,9 +169,9 @@ def test_tb_sweep_shape_checks(C):
 
 @pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
 @pytest.mark.parametrize("first", [False, True])
-@pytest.mark.parametrize("rows,waves", [(2, 4), (2, 8), (4, 4)])
+@pytest.mark.parametrize("rows,waves,kw", [(2, 4, 1), (2, 8, 1), (4, 4, 1), (2, 8, 2)])
 @pytest.mark.parametrize("case", [0, 2, 3])
-def test_tb2_delta_sweep_matches_reference(C, dtype, first, rows, waves, case):
+def test_tb2_delta_sweep_matches_reference(C, dtype, first, rows, waves, kw, case):
     """Increment form: the C level receives d^{m+1}, D receives u^{m+1}; errors of u^m, u^{m+1}."""
     from wave3d.ops import kernels, reference
 
@@ -188,7 +188,8 @@ def test_tb2_delta_sweep_matches_reference(C, dtype, first, rows, waves, case):
     kernels.tb_sweep(A.to(DEV), Dm1.to(DEV), dC, dD, boxes, first=first, cdom=cdom, err_i=ei,
                      tx=tx.to(DEV), ty=ty.to(DEV), tz=tz.to(DEV),
                      coefs_c=(*COEF.values(), COEFS[0], CT[0]), coefs_d=(*COEF.values(), COEFS[1], CT[1]),
-                     err_c=errC, err_d=errD, rows=rows, waves=waves, chunk=chunk, delta=True)
+                     err_c=errC, err_d=errD, rows=rows, waves=waves, chunk=chunk, delta=True,
+                     kwaves=kw)
     torch.cuda.synchronize()
     cast = lambda v: torch.tensor(v, dtype=dtype).item()  # noqa: E731
     h = {k: cast(v) for k, v in COEF.items()}
