@@ -477,6 +477,10 @@ __global__ void __launch_bounds__(kThreads) k_box_copy(const BoxCopyOps<T> ops, 
 
 int march_rows_per_thread() { return 4; }
 
+int march_tile_rows(const KernelVariant& v) {
+    return v.march && !v.flat ? kWaves * v.rows : kNaiveTJ;
+}
+
 bool tile_order_jfirst() {
     static const bool on = [] {
         const char* e = std::getenv("WAVE3D_TILE_ORDER");

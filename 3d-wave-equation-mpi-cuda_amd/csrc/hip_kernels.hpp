@@ -151,6 +151,8 @@ void launch_stamp(u64* ts, int slot, hipStream_t s);
 void launch_encode_keys(const double* v, u64* k, int n, hipStream_t s);
 
 int march_rows_per_thread();
+// j rows of one tile of a single-step kernel variant (march: waves x rows per lane)
+int march_tile_rows(const KernelVariant& v);
 
 // XCD-aware workgroup order for the stencil kernels (device_common.hpp xcd_swizzle);
 // opt-in via env WAVE3D_XCD_SWIZZLE=1 (ablation, not faster on MI355X).

@@ -67,7 +67,8 @@ struct DevRank {
     std::vector<T*> sbuf, rbuf;  // y/z messages only (x messages live in the grid)
     u64* err = nullptr;          // (K+1) * kSlotsPerLayer
     Box compute, error, owned, interior;
-    std::vector<Box> shell;
+    std::vector<Box> shell;      // single step: x shells (flat kernel) first, then y/z shells
+    int shell_x = 0;             // how many of `shell` are x shells
     int zero_mask = 0;
     Wrap wrap;                   // single-step periodic self-wrap (depth 1)
     Wrap wrap2;                  // depth-2 self-wrap (temporal blocking: IC and D layers)
@@ -349,13 +350,24 @@ private:
                     R.pack.zk[f.side] = f.side ? Z : 1;
                 }
             }
-            // interior = compute box minus the layer next to every remote ghost
+            // interior = compute box minus the layer next to every remote ghost. With a tiled
+            // march kernel the j/k shells are widened to whole tiles (its tile rows; k on the
+            // 64-column grid) and run with that kernel; the one-plane x shells (and every shell
+            // of the naive/flat kernels) use the flat one-point-per-thread kernel.
             Box c = R.compute, in = c;
-            if (!R.plan.self_x) in.i0 = std::max(in.i0, 2), in.i1 = std::min(in.i1, X - 1);
-            if (t.nbr[1][0] >= 0) in.j0 = std::max(in.j0, 2);
-            if (t.nbr[1][1] >= 0) in.j1 = std::min(in.j1, Y - 1);
-            if (t.nbr[2][0] >= 0) in.k0 = std::max(in.k0, 2);
-            if (t.nbr[2][1] >= 0) in.k1 = std::min(in.k1, Z - 1);
+            const int TJm = shells_tiled() ? march_tile_rows(kind_) : 1;
+            const int TKm = shells_tiled() ? kTileK : 1;
+            if (!R.plan.self_x) {
+                // the shells hold every plane the exchange sends: the first / last x-rank (or
+                // one x rank messaging itself) sends plane 2 / X-1, skipping the duplicate plane
+                const bool xs = t.dims[0] > 1;
+                in.i0 = std::max(in.i0, 2 + ((t.first(0) || !xs) ? 1 : 0));
+                in.i1 = std::min(in.i1, X - 1 - ((t.last(0) || !xs) ? 1 : 0));
+            }
+            if (t.nbr[1][0] >= 0) in.j0 = std::max(in.j0, std::max(2, c.j0 + TJm));
+            if (t.nbr[1][1] >= 0) in.j1 = std::min(in.j1, std::min(Y - 1, c.j1 - TJm));
+            if (t.nbr[2][0] >= 0) in.k0 = std::max(in.k0, TKm > 1 ? 1 + TKm : 2);
+            if (t.nbr[2][1] >= 0) in.k1 = std::min(in.k1, TKm > 1 ? TKm * ((Z - 1) / TKm) : Z - 1);
             R.interior = in;
             build_tb_plan(R);
             if (tbd_ == 3 && (R.plan.self_x || t.first(0) || t.last(0))) {
@@ -370,9 +382,11 @@ private:
             };
             if (in.empty()) {
                 add(c);
+                R.shell_x = int(R.shell.size());
             } else {
                 add({c.i0, in.i0 - 1, c.j0, c.j1, c.k0, c.k1});
                 add({in.i1 + 1, c.i1, c.j0, c.j1, c.k0, c.k1});
+                R.shell_x = int(R.shell.size());
                 add({in.i0, in.i1, c.j0, in.j0 - 1, c.k0, c.k1});
                 add({in.i0, in.i1, in.j1 + 1, c.j1, c.k0, c.k1});
                 add({in.i0, in.i1, in.j0, in.j1, c.k0, in.k0 - 1});
@@ -598,6 +612,9 @@ private:
             add({in.i0, in.i1, in.j0, in.j1, in.k1 + 1, c.k1});
         }
     }
+
+    // single-step overlap: y/z shells as whole tiles of the march kernel (else flat shells)
+    bool shells_tiled() const { return kind_.march && !kind_.flat; }
 
     bool tb_halo(const DevRank<T>& R) const {
         return !R.tb_sends.empty() || !R.tb_bsends[0].empty() || !R.tb_bsends[1].empty() ||
@@ -1005,13 +1022,21 @@ private:
             } else if (span == 2) {
                 for (auto& R : ranks_) sweep(R, n, s_comp_);
             } else if (overlap_) {
+                // as the two-layer sweep: shells on the comm stream behind the previous halo,
+                // concurrently with the interior; the exchange follows the shells
+                HIP_CHECK(hipEventRecord(ev_layer_, s_comp_));
+                HIP_CHECK(hipStreamWaitEvent(s_comm_, ev_layer_, 0));
+                for (auto& R : ranks_) {
+                    const int nx = R.shell_x, ny = int(R.shell.size()) - nx;
+                    if (nx > 0) step_boxes(R, n, R.shell.data(), nx, naive_, s_comm_);
+                    if (ny > 0)
+                        step_boxes(R, n, R.shell.data() + nx, ny, shells_tiled() ? kind_ : naive_, s_comm_);
+                }
+                HIP_CHECK(hipEventRecord(ev_shell_, s_comm_));
                 for (auto& R : ranks_)
                     if (!R.interior.empty()) step_boxes(R, n, &R.interior, 1, kind_, s_comp_);
-                HIP_CHECK(hipStreamWaitEvent(s_comp_, ev_halo_, 0));
-                for (auto& R : ranks_)
-                    if (!R.shell.empty())
-                        step_boxes(R, n, R.shell.data(), int(R.shell.size()), naive_,
-                                   s_comp_);
+                HIP_CHECK(hipStreamWaitEvent(s_comp_, ev_shell_, 0));
+                comm_follows = true;
             } else {
                 for (auto& R : ranks_) step_boxes(R, n, &R.compute, 1, kind_, s_comp_);
             }
