@@ -33,6 +33,7 @@ CheckpointHeader make_header(const Config& c, const Topology& t, int layer, int 
     h.Lx = c.Lx_is_pi ? -1.0 : c.Lx;
     h.Ly = c.Ly_is_pi ? -1.0 : c.Ly;
     h.Lz = c.Lz_is_pi ? -1.0 : c.Lz;
+    h.scheme = c.delta ? 1 : 0;
     return h;
 }
 
@@ -160,7 +161,8 @@ int read_checkpoint(const std::string& dir, const CheckpointHeader& expect, cons
     bool same = h.N == expect.N && h.K == expect.K && h.nprocs == expect.nprocs &&
                 h.rank == expect.rank && h.elem_size == expect.elem_size &&
                 h.pi_mode == expect.pi_mode && h.ic_mode == expect.ic_mode && h.T == expect.T &&
-                h.Lx == expect.Lx && h.Ly == expect.Ly && h.Lz == expect.Lz && h.layer == expect.layer;
+                h.Lx == expect.Lx && h.Ly == expect.Ly && h.Lz == expect.Lz && h.layer == expect.layer &&
+                h.scheme == expect.scheme;
     for (int a = 0; a < 3; ++a)
         same = same && h.dims[a] == expect.dims[a] && h.coords[a] == expect.coords[a] &&
                h.ext[a] == expect.ext[a];

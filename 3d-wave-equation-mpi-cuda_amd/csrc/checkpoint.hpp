@@ -1,7 +1,8 @@
 // Checkpoint / resume (SURVEY §5.4 — absent in the reference).
 //
-// State needed to resume after layer n: the two newest levels u^{n-1}, u^n (owned nodes
-// only, no ghosts), n itself, and the global per-layer error maxima for layers 0..n.
+// State needed to resume after layer n: the two newest levels u^{n-1}, u^n (increment form:
+// d^n, u^n) — owned nodes only, no ghosts — n itself, and the global per-layer error maxima
+// for layers 0..n.
 // One file per rank and checkpoint layer, `<dir>/ckpt_r<rank>_L<n>.bin`, written to a temp
 // name, fsync'ed, then renamed (and the directory fsync'ed) so a crash never leaves a torn
 // file. Every rank keeps its two newest complete generations: ranks write asynchronously,
@@ -22,7 +23,7 @@
 namespace wave3d {
 
 struct CheckpointHeader {
-    char magic[8] = {'W', '3', 'D', 'C', 'K', 'P', 'T', '1'};
+    char magic[8] = {'W', '3', 'D', 'C', 'K', 'P', 'T', '2'};
     int N = 0, K = 0, nprocs = 0, rank = 0;
     int dims[3] = {0, 0, 0};
     int coords[3] = {0, 0, 0};
@@ -31,6 +32,8 @@ struct CheckpointHeader {
     int elem_size = 0;
     int pi_mode = 0, ic_mode = 0;
     double T = 0, Lx = 0, Ly = 0, Lz = 0;
+    int scheme = 0;  // 0 leapfrog: levels u^{n-1}, u^n; 1 increment form: d^n, u^n
+    int pad = 0;
 };
 
 CheckpointHeader make_header(const Config& c, const Topology& t, int layer, int elem_size);

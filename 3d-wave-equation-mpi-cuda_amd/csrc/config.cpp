@@ -195,8 +195,6 @@ Config parse_cli(const std::vector<std::string>& a) {
         }
     }
     W3D_REQUIRE(c.repeat >= 1 && c.warmup >= 0, "bad --repeat/--warmup");
-    W3D_REQUIRE(!c.delta || (c.checkpoint_every == 0 && c.resume_dir.empty()),
-                "--scheme delta does not support checkpoints yet");
     W3D_REQUIRE(c.checkpoint_every == 0 || !c.checkpoint_dir.empty(),
                 "--checkpoint-every needs --checkpoint-dir");
     if (c.fault.empty()) {

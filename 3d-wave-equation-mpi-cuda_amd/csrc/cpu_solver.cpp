@@ -471,7 +471,8 @@ private:
         }
         for (auto& R : ranks_) {
             CheckpointHeader h = make_header(cfg_, R.topo, n, sizeof(T));
-            write_checkpoint(cfg_.checkpoint_dir, h, host_level(R, (n + 2) % 3),
+            // leapfrog keeps u^{n-1} (slot (n+2)%3), the increment form d^n (slot (n+1)%3)
+            write_checkpoint(cfg_.checkpoint_dir, h, host_level(R, (n + (cfg_.delta ? 1 : 2)) % 3),
                              host_level(R, n % 3), a, r);
             prune_checkpoints(cfg_.checkpoint_dir, R.topo.rank, 2);
         }
@@ -494,7 +495,8 @@ private:
         const int n = agree_resume_layer(cfg_.resume_dir, lr, ext_);  // same layer on every rank
         for (auto& R : ranks_) {
             CheckpointHeader h = make_header(cfg_, R.topo, n, sizeof(T));
-            read_checkpoint(cfg_.resume_dir, h, host_level(R, (n + 2) % 3), host_level(R, n % 3),
+            read_checkpoint(cfg_.resume_dir, h, host_level(R, (n + (cfg_.delta ? 1 : 2)) % 3),
+                            host_level(R, n % 3),
                             ckpt_abs_, ckpt_rel_);
         }
         // refill ghosts of both levels with one exchange each

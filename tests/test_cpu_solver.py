@@ -120,6 +120,22 @@ def test_checkpoint_resume_bitwise(C, tmp_path):
         _solve(wave3d.WaveProblem(20, timesteps=15), ranks=4, resume=str(tmp_path))
 
 
+def test_checkpoint_resume_delta_scheme(C, tmp_path):
+    """The increment form checkpoints d^n with u^n and resumes bitwise; a leapfrog run refuses
+    those files (the header records the scheme)."""
+    import wave3d
+
+    p = wave3d.WaveProblem(20, timesteps=14, ic="shifted", dtype="fp32", scheme="delta")
+    full = _solve(p, ranks=2)
+    _solve(p, ranks=2, checkpoint_every=6, checkpoint_dir=str(tmp_path))
+    res = _solve(p, ranks=2, resume=str(tmp_path))
+    assert res.extra["resumed_from"] == 12
+    assert res.max_abs == full.max_abs and res.max_rel == full.max_rel
+    with pytest.raises(Exception):
+        _solve(wave3d.WaveProblem(20, timesteps=14, ic="shifted", dtype="fp32"), ranks=2,
+               resume=str(tmp_path))
+
+
 def test_checkpoint_generations_and_agreed_resume(C, tmp_path):
     """Two complete generations per rank are kept; a rank whose newest file is missing (a crash
     while writing it) makes every rank resume from the newest layer they all have."""

@@ -329,3 +329,20 @@ def test_delta_scheme_fp32_accuracy_gpu(C):
     lf = _solve(wave3d.WaveProblem(128, timesteps=400, dtype="fp32")).linf_abs
     d = _solve(wave3d.WaveProblem(128, timesteps=400, dtype="fp32", scheme="delta")).linf_abs
     assert d < 1.2 * e64 and lf > 20 * d
+
+
+@pytest.mark.parametrize("ranks,dims", [(0, None), (2, [2, 1, 1]), (8, [2, 2, 2])])
+def test_delta_scheme_checkpoint_resume(C, tmp_path, ranks, dims):
+    """Increment form on the HIP sweep: checkpoint (d^n, u^n) after layer 12, resume, equal to
+    the uninterrupted run bit for bit (and to the OpenMP oracle)."""
+    import wave3d
+
+    p = wave3d.WaveProblem(29, Lx=1.3, Ly="pi", Lz=2.0, timesteps=16, ic="shifted", dtype="fp32",
+                           scheme="delta")
+    full = _solve(p, ranks=ranks, dims=dims)
+    _solve(p, ranks=ranks, dims=dims, checkpoint_every=6, checkpoint_dir=str(tmp_path))
+    res = _solve(p, ranks=ranks, dims=dims, resume=str(tmp_path))
+    assert res.extra["resumed_from"] == 12
+    assert res.max_abs == full.max_abs and res.max_rel == full.max_rel
+    ref = _solve(p, backend="cpu", threads=4)
+    assert full.max_abs == ref.max_abs
