@@ -6,7 +6,10 @@
 //   Transport                      subclassable from Python (e.g. torch.distributed/gloo)
 //   k_* functions                  the individual HIP kernels, for numerics tests
 #include <hip/hip_runtime.h>
+#include <pybind11/functional.h>
 #include <pybind11/pybind11.h>
+
+#include <chrono>
 #include <pybind11/stl.h>
 
 #include "checkpoint.hpp"
@@ -380,6 +383,20 @@ PYBIND11_MODULE(_wave3d_C, m) {
         Topology::dims_create(n, d);
         return std::vector<int>{d[0], d[1], d[2]};
     });
+    // host-side watchdog probe for tests: the device "finishes" after `done_after_s`; progress
+    // grows every poll until `progress_until_s`, then stalls; returns the wait or raises
+    m.def("watchdog_probe", [](double limit_s, double done_after_s, double progress_until_s) {
+        using clk = std::chrono::steady_clock;
+        const auto t0 = clk::now();
+        auto el = [&] { return std::chrono::duration<double>(clk::now() - t0).count(); };
+        long p = 0;
+        const std::function<long()> prog = [&] { return el() < progress_until_s ? ++p : p; };
+        bool aborted = false;
+        py::gil_scoped_release nogil;
+        watch_until([&] { return el() >= done_after_s; }, [] { return std::string(); }, &prog,
+                    limit_s, [&] { aborted = true; }, "probe");
+        return el();
+    }, py::arg("limit_s"), py::arg("done_after_s"), py::arg("progress_until_s"));
     m.def("checkpoint_layers", &checkpoint_layers, py::arg("dir"), py::arg("rank"),
           "Layers with a complete checkpoint file of `rank` in `dir` (ascending).");
     m.def("encode_max_key", &encode_max_key);

@@ -1,6 +1,43 @@
 #include "halo.hpp"
 
+#include <chrono>
+#include <cstdlib>
+#include <thread>
+
 namespace wave3d {
+
+double watchdog_limit_s() {
+    static const double limit = [] {
+        const char* e = std::getenv("WAVE3D_WATCHDOG_S");
+        return e ? std::atof(e) : 120.0;
+    }();
+    return limit;
+}
+
+void watch_until(const std::function<bool()>& done, const std::function<std::string()>& async_error,
+                 const std::function<long()>* progress, double limit_s,
+                 const std::function<void()>& abort, const std::string& what) {
+    using clk = std::chrono::steady_clock;
+    auto t0 = clk::now();
+    long seen = progress ? (*progress)() : 0;
+    for (int spin = 0;; ++spin) {
+        if (done()) return;
+        const std::string err = async_error();
+        const auto now = clk::now();
+        if (progress && (spin & 63) == 0) {
+            const long p = (*progress)();
+            if (p != seen) seen = p, t0 = now;  // the device moved on: restart the clock
+        }
+        const double el = std::chrono::duration<double>(now - t0).count();
+        if (!err.empty() || (limit_s > 0 && el > limit_s)) {
+            abort();
+            throw Error(!err.empty() ? what + " async error: " + err
+                                     : what + " watchdog: no progress for " + std::to_string(int(el)) +
+                                           " s (WAVE3D_WATCHDOG_S), communicator aborted");
+        }
+        if (spin > 1000) std::this_thread::sleep_for(std::chrono::microseconds(200));
+    }
+}
 
 HaloPlan make_halo_plan(const Topology& t, i64 x_plane, int row, bool self_msg) {
     HaloPlan p;

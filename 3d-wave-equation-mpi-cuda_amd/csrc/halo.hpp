@@ -50,6 +50,17 @@ struct Message {
     size_t bytes = 0;
 };
 
+// Watchdog loop shared by the device transports: polls `done` until it returns
+// true; `async_error` returns a non-empty message when the communicator failed; `progress`
+// (optional) grows while the device makes progress, and the clock restarts whenever it does.
+// On an error or `limit_s` seconds (> 0) without progress it calls `abort` and throws
+// wave3d::Error naming the cause. Host-only (unit-tested on the CPU).
+void watch_until(const std::function<bool()>& done, const std::function<std::string()>& async_error,
+                 const std::function<long()>* progress, double limit_s,
+                 const std::function<void()>& abort, const std::string& what);
+// WAVE3D_WATCHDOG_S, default 120 s (below the benchmark driver's timeout)
+double watchdog_limit_s();
+
 // A transport moves the messages of one exchange. Device transports order the operation
 // on `stream` (a hipStream_t) and return without host synchronisation; host transports
 // complete before returning.

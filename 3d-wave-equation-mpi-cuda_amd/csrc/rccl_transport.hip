@@ -113,41 +113,25 @@ void RcclTransport::check_async() const {
     if (st != ncclSuccess) throw Error(std::string("RCCL async error: ") + ncclGetErrorString(st));
 }
 
-double watchdog_limit_s() {
-    static const double limit = [] {
-        const char* e = std::getenv("WAVE3D_WATCHDOG_S");
-        return e ? std::atof(e) : 120.0;
-    }();
-    return limit;
-}
-
 bool RcclTransport::wait_stream(void* stream, const std::function<long()>* progress) {
     hipStream_t s = static_cast<hipStream_t>(stream);
-    const double limit = watchdog_limit_s();
-    auto t0 = std::chrono::steady_clock::now();
-    long seen = progress ? (*progress)() : 0;
-    for (int spin = 0;; ++spin) {
-        const hipError_t q = hipStreamQuery(s);
-        if (q == hipSuccess) break;
-        if (q != hipErrorNotReady) HIP_CHECK_T(q);
-        ncclResult_t st = ncclSuccess;
-        NCCL_CHECK(ncclCommGetAsyncError(impl_->comm, &st));
-        const auto now = std::chrono::steady_clock::now();
-        if (progress && (spin & 63) == 0) {
-            const long p = (*progress)();
-            if (p != seen) seen = p, t0 = now;  // the device moved on: restart the clock
-        }
-        const double el = std::chrono::duration<double>(now - t0).count();
-        if (st != ncclSuccess || (limit > 0 && el > limit)) {
+    watch_until(
+        [&] {
+            const hipError_t q = hipStreamQuery(s);
+            if (q != hipErrorNotReady) HIP_CHECK_T(q);
+            return q == hipSuccess;
+        },
+        [&] {
+            ncclResult_t st = ncclSuccess;
+            NCCL_CHECK(ncclCommGetAsyncError(impl_->comm, &st));
+            return st == ncclSuccess ? std::string() : std::string(ncclGetErrorString(st));
+        },
+        progress, watchdog_limit_s(),
+        [&] {
             (void)ncclCommAbort(impl_->comm);
             impl_->comm = nullptr;
-            throw Error(st != ncclSuccess
-                            ? std::string("RCCL async error: ") + ncclGetErrorString(st)
-                            : "RCCL watchdog: no progress for " + std::to_string(int(el)) +
-                                  " s (WAVE3D_WATCHDOG_S), communicator aborted");
-        }
-        if (spin > 1000) std::this_thread::sleep_for(std::chrono::microseconds(200));
-    }
+        },
+        "RCCL");
     return true;
 }
 

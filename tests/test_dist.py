@@ -103,3 +103,14 @@ def test_rccl_self_send(C, single_cpu, kernel, overlap):
     assert r["exchange_ms"] > 0  # halo messages were timed on the stream
     assert r["max_abs"] == single_cpu["max_abs"] and r["max_rel"] == single_cpu["max_rel"]
 
+
+
+def test_watchdog_is_progress_based(C):
+    """The transport watchdog (halo.cpp watch_until, used by RcclTransport::wait_stream) measures
+    time since the device last made progress, not since the wait began: a wait that keeps
+    progressing outlives the limit, a stalled one is aborted with a message naming the cause."""
+    # progress for 0.6 s, done at 0.7 s, limit 0.3 s: never 0.3 s without progress -> no abort
+    assert 0.69 < C.watchdog_probe(0.3, 0.7, 0.65) < 2.0
+    # progress stalls at 0.1 s, never done: aborted ~0.3 s later
+    with pytest.raises(Exception, match="no progress"):
+        C.watchdog_probe(0.3, 100.0, 0.1)
