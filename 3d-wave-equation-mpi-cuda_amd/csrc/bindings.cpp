@@ -200,10 +200,24 @@ void k_tb2_dense(int rows, int waves, int nwk, bool delta, bool first, uintptr_t
     W3D_REQUIRE(v.G >= 2, "k_tb2 needs ghost depth >= 2");
     std::vector<Box> bx;
     for (auto& b : boxes) bx.push_back(tobox(b));
-    launch_tb2<T>(rows, waves, 0, nwk, delta, first, P<T>(A) + o, P<T>(B) + o, P<T>(Cc) + o, P<T>(D) + o, v,
-                  bx.data(), int(bx.size()), tobox(cdom), ei0, ei1, towrap(wrapC), towrap(wrapD),
-                  SeamAlias<T>{}, P<T>(tx), P<T>(ty), P<T>(tz), tocoefs(cC), tocoefs(cD),
-                  P<u64>(errC), P<u64>(errD), chunk, (hipStream_t)stream);
+    // the kernel reads sx*sy from a product table (the solver builds it once per run)
+    const hipStream_t s = (hipStream_t)stream;
+    T* txy = nullptr;
+    if (hipMalloc(&txy, txy_elems(v.X, v.Y) * sizeof(T)) != hipSuccess) throw Error("k_tb2: hipMalloc failed");
+    try {
+        launch_txy<T>(txy, P<T>(tx), P<T>(ty), v.X, v.Y, s);
+        launch_tb2<T>(rows, waves, 0, nwk, delta, first, P<T>(A) + o, P<T>(B) + o, P<T>(Cc) + o, P<T>(D) + o, v,
+                      bx.data(), int(bx.size()), tobox(cdom), ei0, ei1, towrap(wrapC), towrap(wrapD),
+                      SeamAlias<T>{}, txy, P<T>(tz), tocoefs(cC), tocoefs(cD),
+                      P<u64>(errC), P<u64>(errD), chunk, s);
+    } catch (...) {
+        (void)hipStreamSynchronize(s);
+        (void)hipFree(txy);
+        throw;
+    }
+    const hipError_t e = hipStreamSynchronize(s);
+    (void)hipFree(txy);
+    if (e != hipSuccess) throw Error(std::string("k_tb2: ") + hipGetErrorString(e));
 }
 
 // One three-layer sweep (k_tb3): C = u^m (errors only), D = u^{m+1}, E = u^{m+2}.

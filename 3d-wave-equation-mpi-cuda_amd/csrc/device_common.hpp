@@ -49,42 +49,73 @@ __device__ __forceinline__ T wave_max(T v) {
     return v;
 }
 
+// m = max(m, |d|) as one v_max with an abs source modifier. fmax() of a loop-carried value
+// costs two extra canonicalising v_max per node (plus a v_and for the |.|); the raw
+// instruction in IEEE mode already returns the other operand for a quiet-NaN input, and every
+// NaN here is an arithmetic result (quiet) — the reference's NaN-ignoring `if (e > m) m = e`.
+__device__ __forceinline__ double max_abs(double m, double d) {
+    double r;
+    asm("v_max_f64 %0, %1, |%2|" : "=v"(r) : "v"(m), "v"(d));
+    return r;
+}
+__device__ __forceinline__ float max_abs(float m, float d) {
+    float r;
+    asm("v_max_f32_e64 %0, %1, |%2|" : "=v"(r) : "v"(m), "v"(d));
+    return r;
+}
+
+// up ? |t| : k without materialising |t|: a double select is two 32-bit v_cndmask, and the
+// sign bit lives in the high word, whose select takes |.| as a free source modifier.
+__device__ __forceinline__ double pick_abs(bool up, double k, double t) {
+    const u64 kb = __builtin_bit_cast(u64, k), tb = __builtin_bit_cast(u64, t);
+    const unsigned lo = up ? unsigned(tb) : unsigned(kb);
+    unsigned hi;
+    asm("v_cndmask_b32_e64 %0, %1, |%2|, %3"
+        : "=v"(hi)
+        : "v"(unsigned(kb >> 32)), "v"(unsigned(tb >> 32)), "s"(__builtin_amdgcn_ballot_w64(up)));
+    return __builtin_bit_cast(double, (u64(hi) << 32) | lo);
+}
+__device__ __forceinline__ float pick_abs(bool up, float k, float t) {
+    float r;
+    asm("v_cndmask_b32_e64 %0, %1, |%2|, %3" : "=v"(r) : "v"(k), "v"(t), "s"(__builtin_amdgcn_ballot_w64(up)));
+    return r;
+}
+
 // Running maximum of the relative error |u-f|/|f| without a division per node: the argmax is
 // tracked exactly as the pair (num, den) by comparing num'*den vs num*den' through products
 // split into RN value + exact FMA residual, and the one IEEE division happens at the end.
 // RN is monotone, so value() = RN(max exact quotient) = max of the reference's RN quotients
 // (mpi_new.cpp:341-344): bitwise equal, including its NaN-ignoring `>` and the x/0 = inf case
 // (exact as long as the products are normal numbers, i.e. |errors| and |f| above ~1e-150).
+// add() takes the signed d = u - f and f: the |.| are source modifiers of the products and of
+// the selects (pick_abs), so num, den hold |d|, |f| without a v_and per node.
 template <class T>
 struct RelArg {
     T num = T(kErrInit), den = T(1);
-    __device__ __forceinline__ void add(T ea, T fa) {
+    __device__ __forceinline__ void add(T d, T f) {
 #pragma clang fp contract(off)
-        const T p1 = ea * den, p2 = num * fa;
+        const T p1 = absval(d) * den, p2 = num * absval(f);
         bool up = p1 > p2;
         // exact tie-break on the FMA residuals only where the rounded products tie (rare:
         // mirror-symmetric nodes); the wave skips the block when no lane ties
-        if (__builtin_expect(p1 == p2, 0)) up = fma_t(ea, den, -p1) > fma_t(num, fa, -p2);
-        if (up) num = ea, den = fa;
+        if (__builtin_expect(p1 == p2, 0)) up = fma_t(absval(d), den, -p1) > fma_t(num, absval(f), -p2);
+        num = pick_abs(up, num, d);
+        den = pick_abs(up, den, f);
     }
     __device__ __forceinline__ T value() const { return num / den; }
 };
 
-__device__ __forceinline__ double fmax_t(double a, double b) { return __builtin_fmax(a, b); }
-__device__ __forceinline__ float fmax_t(float a, float b) { return __builtin_fmaxf(a, b); }
-
 // Per node: |u - f| into the running maximum and the relative-error argmax, and u into `chk`.
-// The maximum is v_max (IEEE maxNum): a NaN error is ignored exactly like the reference's
-// `if (e > m) m = e` (mpi_new.cpp:343-344; errors are arithmetic results, never signalling
-// NaNs). `chk` is the sum of the layer's values: non-finite iff some value was NaN/Inf (or
-// the values overflow a double, i.e. the run diverged anyway) — one add per node instead of
-// a compare-and-or; commit_errors() turns it into the nonfinite flag.
+// The maximum ignores a NaN error exactly like the reference's `if (e > m) m = e`
+// (mpi_new.cpp:343-344; max_abs). `chk` is the sum of the layer's values: non-finite iff some
+// value was NaN/Inf (or the values overflow a double, i.e. the run diverged anyway) — one add
+// per node instead of a compare-and-or; commit_errors() turns it into the nonfinite flag.
 template <class T>
 __device__ __forceinline__ void accumulate_error_dev(T u, T f, T& mabs, RelArg<T>& mrel) {
 #pragma clang fp contract(off)
-    const T ea = absval(u - f);
-    mabs = fmax_t(mabs, ea);
-    mrel.add(ea, absval(f));
+    const T d = u - f;
+    mabs = max_abs(mabs, d);
+    mrel.add(d, f);
 }
 
 // Workgroup reduction of the running maxima + one atomic per slot (race-free, no

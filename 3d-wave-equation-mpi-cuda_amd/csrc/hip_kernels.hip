@@ -481,12 +481,15 @@ int march_tile_rows(const KernelVariant& v) {
     return v.march && !v.flat ? kWaves * v.rows : kNaiveTJ;
 }
 
-bool tile_order_jfirst() {
-    static const bool on = [] {
+int tile_order() {
+    static const int order = [] {
         const char* e = std::getenv("WAVE3D_TILE_ORDER");
-        return !(e && e[0] == 'k');
+        if (!e || !*e) return 1;
+        if (e[0] == 'k') return 0;
+        if (e[0] == 'b') return 2;
+        return 1;
     }();
-    return on;
+    return order;
 }
 
 bool xcd_swizzle_enabled() {
@@ -699,6 +702,26 @@ void launch_faces(T* u, const GridView& gv, const FaceOp<T>* ops, int nops, bool
                        to_buf);
     HIP_OK(hipGetLastError());
 }
+
+namespace {
+template <class T>
+__global__ void k_txy(T* out, const T* tx, const T* ty, int X, int Y, size_t n) {
+    const size_t q = size_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (q >= n) return;
+    const size_t pj = size_t(Y + 2), used = size_t(X + 2) * pj;
+    // the analytic product's first factor, rounded exactly as stencil_math analytic()
+    out[q] = q < used ? tx[q / pj] * ty[q % pj] : T(0);
+}
+}  // namespace
+
+template <class T>
+void launch_txy(T* out, const T* tx, const T* ty, int X, int Y, hipStream_t s) {
+    const size_t n = txy_elems(X, Y);
+    hipLaunchKernelGGL(k_txy<T>, dim3(unsigned((n + 255) / 256)), dim3(256), 0, s, out, tx, ty, X, Y, n);
+    HIP_OK(hipGetLastError());
+}
+template void launch_txy<double>(double*, const double*, const double*, int, int, hipStream_t);
+template void launch_txy<float>(float*, const float*, const float*, int, int, hipStream_t);
 
 void launch_init_err(u64* err, int layers, hipStream_t s) {
     const int n = layers * 3;

@@ -157,11 +157,12 @@ int march_tile_rows(const KernelVariant& v);
 // XCD-aware workgroup order for the stencil kernels (device_common.hpp xcd_swizzle);
 // opt-in via env WAVE3D_XCD_SWIZZLE=1 (ablation, not faster on MI355X).
 bool xcd_swizzle_enabled();
-// Temporal-blocking tile order: j-neighbour tiles at consecutive block ids, so k-neighbours are
-// a multiple of 8 ids apart and share an XCD (their halo lines then hit that XCD's L2: -17 %
-// memory-side reads, profiles/tile_order_r2.txt). Default; WAVE3D_TILE_ORDER=k restores the
-// k-fastest order (A/B switch).
-bool tile_order_jfirst();
+// Temporal-blocking tile order (env WAVE3D_TILE_ORDER): 1 = "j" (default): j-neighbour tiles at
+// consecutive block ids, so k-neighbours are a multiple of 8 ids apart and share an XCD (their
+// halo lines then hit that XCD's L2: -17 % memory-side reads, profiles/tile_order_r2.txt);
+// 0 = "k": k-fastest; 2 = "band": XCD x (block id mod 8) owns a band of tiles_j/8 adjacent tile
+// rows for every k, so j-neighbours inside a band share its L2 as well.
+int tile_order();
 
 // Temporal blocking: one sweep computes layers m (C) and m+1 (D) from A = u^{m-1} and
 // B = u^{m-2} (unused when m == 1), D-boxes as for launch_step. C is evaluated on a one-node
@@ -185,11 +186,20 @@ bool tb2_supported(int rows, int waves, int occ = 0, int nwk = 1);
 // delta: increment form — B holds d^{m-1}; C receives d^{m+1} (planes of D, with C's wrap
 // planes), D receives u^{m+1}; u^m is formed in registers for its errors only.
 bool tb2_delta_supported(int rows, int waves, int nwk = 1);
+// `txy` = the sx*sy product table of launch_txy (X, Y of gv).
 template <class T>
 void launch_tb2(int rows, int waves, int occ, int nwk, bool delta, bool first, const T* A, const T* B, T* C, T* D, const GridView& gv,
                 const Box* boxes, int nbox, const Box& cdom, int ei0, int ei1, const Wrap& wrapC,
-                const Wrap& wrapD, const SeamAlias<T>& alias, const T* tx, const T* ty,
-                const T* tz, const StepCoefs& cC, const StepCoefs& cD, u64* errC, u64* errD,
+                const Wrap& wrapD, const SeamAlias<T>& alias, const T* txy, const T* tz,
+                const StepCoefs& cC, const StepCoefs& cD, u64* errC, u64* errD,
                 int chunk, hipStream_t s);
+
+// Analytic-product table of the temporal-blocking kernels: out[i*(Y+2) + j] = RN(tx[i]*ty[j])
+// for i in 0..X+1, j in 0..Y+1 (tables of X+2 / Y+2 entries), then txy_pad zero elements (rows
+// past the last are read, unused, by masked waves). Holds txy_elems(X, Y) elements.
+constexpr int kTxyPad = 256;
+inline size_t txy_elems(int X, int Y) { return size_t(X + 2) * size_t(Y + 2) + kTxyPad; }
+template <class T>
+void launch_txy(T* out, const T* tx, const T* ty, int X, int Y, hipStream_t s);
 
 }  // namespace wave3d

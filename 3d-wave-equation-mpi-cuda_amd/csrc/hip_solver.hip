@@ -63,6 +63,7 @@ struct DevRank {
     i64 plane_off = 0;                                 // g - (start of logical plane 0)
     size_t elems = 0;                                  // allocation per level
     T *tx = nullptr, *ty = nullptr, *tz = nullptr;
+    T* txy = nullptr;  // sx*sy table of the temporal-blocking sweep (launch_txy)
     HaloPlan plan;
     std::vector<T*> sbuf, rbuf;  // y/z messages only (x messages live in the grid)
     u64* err = nullptr;          // (K+1) * kSlotsPerLayer
@@ -298,6 +299,11 @@ private:
             R.tx = upload(tabx, X, R.topo.off[0]);
             R.ty = upload(taby, Y, R.topo.off[1]);
             R.tz = upload(tabz, Z, R.topo.off[2]);
+            if (tb_) {
+                HIP_CHECK(hipMalloc(&R.txy, txy_elems(X, Y) * sizeof(T)));
+                launch_txy<T>(R.txy, R.tx, R.ty, X, Y, nullptr);
+                HIP_CHECK(hipDeviceSynchronize());
+            }
             R.plan = make_halo_plan(R.topo, R.gv.si, Z + 2, xself_);
             if (R.plan.self_x) W3D_REQUIRE(X >= 3, "periodic self-wrap needs >= 3 x planes");
             R.sbuf.assign(R.plan.sends.size(), nullptr);
@@ -406,6 +412,7 @@ private:
             (void)hipFree(R.tx);
             (void)hipFree(R.ty);
             (void)hipFree(R.tz);
+            (void)hipFree(R.txy);
             for (auto* p : R.sbuf) (void)hipFree(p);
             for (auto* p : R.rbuf) (void)hipFree(p);
             (void)hipFree(R.err);
@@ -727,7 +734,7 @@ private:
         }
         if (!boxes) boxes = &R.compute, nbox = 1;
         launch_tb2<T>(tb_rows_, tb_waves_, tb_occ_, tb_nwk_, cfg_.delta, m == 1, A, B, R.g[lvl(m)], R.g[lvl(m + 1)], R.gv, boxes, nbox,
-                      R.cdom, R.error.i0, R.error.i1, R.wrap, R.wrap2, al, R.tx, R.ty, R.tz,
+                      R.cdom, R.error.i0, R.error.i1, R.wrap, R.wrap2, al, R.txy, R.tz,
                       coefs(m), coefs(m + 1), R.err + size_t(m) * kSlotsPerLayer,
                       R.err + size_t(m + 1) * kSlotsPerLayer, cfg_.chunk, s);
     }

@@ -34,12 +34,16 @@ namespace {
 template <class T>
 struct TbParams {
     int xcd;     // XCD-aware tile order (xcd_swizzle)
-    int jfirst;  // tile order: j-neighbours at consecutive block ids (k-neighbours share an XCD)
-    const T* A;
-    const T* B;
-    T* C;
-    T* D;
-    i64 si;
+    int order;   // tile order (tile_order(): 0 k-fastest, 1 j-fastest, 2 XCD bands)
+    // Level bases pre-biased on the host so that plane i's block starts at
+    // base + (i + pbias) * pbytes with i + pbias >= 0: one 32x32->64-bit product per descriptor
+    // instead of a signed 64-bit plane-index multiply (~half the scalar instructions per plane).
+    const char* A;
+    const char* B;
+    char* C;
+    char* D;
+    unsigned pbytes;  // plane bytes (< 4 GiB: one buffer descriptor per plane)
+    int pbias;
     int sj;
     int poff;                    // see GridView::poff
     int jmin, jmax, kmin, kmax;  // storage bounds (logical)
@@ -52,10 +56,12 @@ struct TbParams {
     int wc_lo[2], wc_hi[2], wc_sh[2];
     int wd_lo[2], wd_hi[2], wd_sh[2];
     int an_i, ap_i;
-    const T* an;
+    const T* an;  // seam alias planes, block starts (logical (i,0,0) - poff)
     const T* ap;
-    const T* tx;
-    const T* ty;
+    // txy[i * tpj + j] = RN(tx[i] * ty[j]) (launch_txy): the analytic value
+    // ((sx*sy)*sz)*ct is then two multiplies per node with the reference's rounding
+    const T* txy;
+    int tpj;
     const T* tz;
     T hx2, hy2, hz2, coefC, coefD, ctC, ctD;
     T yx2, yy2, yz2;  // RN(1/h^2): correctly rounded constant division
@@ -102,7 +108,16 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WP
     const BoxLaunch Bx = p.box[b];
     int local = bid - Bx.block_begin;
     int tk, tj;
-    if (p.jfirst) {
+    if (p.order == 2 && Bx.tiles_j % kXcds == 0) {
+        // block ids dealt round-robin over the XCDs: x = id mod 8 runs tile rows
+        // [x*hb, x*hb + hb) of every k-tile and chunk, j-fastest inside its band
+        const int hb = Bx.tiles_j / kXcds, x = local % kXcds;
+        local /= kXcds;
+        tj = x * hb + local % hb;
+        local /= hb;
+        tk = local % Bx.tiles_k;
+        local /= Bx.tiles_k;
+    } else if (p.order) {
         tj = local % Bx.tiles_j;
         local /= Bx.tiles_j;
         tk = local % Bx.tiles_k;
@@ -122,33 +137,55 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WP
     const int w8 = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int w = w8 % NWJ;                 // wave's row band
     const int kl = (w8 / NWJ) * kTK + lane;  // column within the tile
-    const i64 si = p.si;
     const int sj = p.sj;
-    const unsigned pbytes = unsigned(si) * ES;
+    const unsigned pbytes = p.pbytes;
 
     auto inb = [&](int j, int k) { return j >= p.jmin && j <= p.jmax && k >= p.kmin && k <= p.kmax; };
     auto incd = [&](int j, int k) { return j >= p.cj0 && j <= p.cj1 && k >= p.ck0 && k <= p.ck1; };
     // byte offset of (j,k) inside a plane block, or kOOB
     auto boff = [&](int j, int k, bool ok) { return ok ? unsigned(j * sj + k + p.poff) * ES : kOOB; };
-    // descriptor of logical plane i of an array (wave-uniform)
-    auto prs = [&](const T* base, int i) { return plane_rsrc(base + (i64(i) * si - p.poff), pbytes); };
+    // descriptor of logical plane i of a level (wave-uniform; `nb` bytes: 0 = loads return 0)
+    auto prs = [&](const char* base, int i, unsigned nb) {
+        return plane_rsrc(base + u64(unsigned(i + p.pbias)) * pbytes, nb);
+    };
 
     // ---- own nodes (D and C) ----------------------------------------------------------
     const int k = kb + kl;
+    const int jrow = jt + w * R;  // first row of this wave (wave-uniform)
     unsigned oa[R], ob[R], os[R];  // A-load, B-load, store offsets (kOOB when masked)
     bool ovalid[R], ocd[R];
-    T oty[R];
 #pragma unroll
     for (int r = 0; r < R; ++r) {
-        const int j = jt + w * R + r;
+        const int j = jrow + r;
         ocd[r] = incd(j, k);
         ovalid[r] = k >= Bx.k0 && k <= Bx.k1 && j <= Bx.j1;
         oa[r] = boff(j, k, inb(j, k));
         ob[r] = boff(j, k, !FIRST && inb(j, k) && ocd[r]);
         os[r] = boff(j, k, ovalid[r]);
-        oty[r] = ldconst(p.ty, min(j, Bx.j1));  // wave-uniform row: a scalar load, SGPRs
     }
     const T otz = (k >= Bx.k0 && k <= Bx.k1) ? p.tz[k] : T(0);
+    // rows of this wave in the sx*sy table (launch_txy pads past the last row, so rows beyond
+    // the box — never used, their lanes are masked — are in-bounds reads)
+    const T* const txw = p.txy + jrow;
+
+    // Rare per-plane events of this work item as wave-uniform bits, so the common plane pays
+    // one scalar test for all of them: C / D self-wrap ranges met (1, 2 / 4, 8), seam alias
+    // plane met (16). Own planes [ib, ie]: C stored at i, D at i - 1.
+    int rare = 0;
+#pragma unroll
+    for (int g = 0; g < 2; ++g) {
+        if (p.wc_lo[g] <= ie && p.wc_hi[g] >= ib) rare |= 1 << g;
+        if (p.wd_lo[g] <= ie && p.wd_hi[g] >= ib) rare |= 4 << g;
+    }
+    if ((p.an_i >= ib - 1 && p.an_i <= ie + 1) || (p.ap_i >= ib - 1 && p.ap_i <= ie + 1)) rare |= 16;
+    rare = __builtin_amdgcn_readfirstlane(rare);
+    // error planes of this work item: [e0, e0 + espan] (none: e0 far below every plane)
+    const int e0r = max(ib, p.ei0), e1r = min(ie, p.ei1);
+    const int e0 = e1r >= e0r ? e0r : INT_MIN / 2;
+    const unsigned espan = e1r >= e0r ? unsigned(e1r - e0r) : 0u;
+    const unsigned ospan = unsigned(ie - ib);
+    auto own = [&](int i) { return unsigned(i - ib) <= ospan; };
+    auto eplane = [&](int i) { return unsigned(i - e0) <= espan; };
 
     // ---- C-ring node of this thread (rolling A, C into the LDS tile only) --------------
     // rows jt-1 / jt+TJ over cols kb..kb+TK-1, then cols kb-1 / kb+TK over rows jt-1..jt+TJ
@@ -187,8 +224,8 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WP
     T dl[DELTA ? 2 : 1][R];  // increment form: d^m of planes i (H0) and i-1 (H1)
     T ra[4], rb[2], ua[4];
     {
-        const auto r0 = prs(p.A, ib - 2), r1 = prs(p.A, ib - 1), r2 = prs(p.A, ib);
-        const auto rB = prs(p.B, ib - 1);
+        const auto r0 = prs(p.A, ib - 2, pbytes), r1 = prs(p.A, ib - 1, pbytes), r2 = prs(p.A, ib, pbytes);
+        const auto rB = prs(p.B, ib - 1, pbytes);
 #pragma unroll
         for (int r = 0; r < R; ++r) {
             a[0][r] = bld<T>(r0, oa[r]);
@@ -215,6 +252,31 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WP
     RelArg<T> mr1, mr2;
     T chk1 = T(0), chk2 = T(0);
 
+    // errors and finiteness sum of one own plane i of a layer (values v[r]); the uniform plane
+    // test outside the per-lane row masks keeps it a scalar branch
+    auto errors = [&](const T(&v)[R], const int i, const T ct, T& ma, RelArg<T>& mr, T& chk) {
+        if constexpr (ABL == 1) return;
+        if (eplane(i)) {
+            const T* const trow = txw + i * p.tpj;
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                if (!ovalid[r]) continue;
+                chk += v[r];
+                const T f = (ldconst(trow, r) * otz) * ct;  // = ((sx*sy)*sz)*ct, stencil_math analytic
+                if constexpr (ABL == 2) {
+                    const T e = absval(v[r] - f);
+                    if (e > ma) ma = e;
+                } else {
+                    accumulate_error_dev(v[r], f, ma, mr);
+                }
+            }
+        } else {
+#pragma unroll
+            for (int r = 0; r < R; ++r)
+                if (ovalid[r]) chk += v[r];
+        }
+    };
+
     // prefetch A(i+2) (own, both rings), B(i+1); on the last plane the
     // descriptors get 0 records, so the loads return 0 without touching memory (uniform,
     // no per-lane masking)
@@ -224,8 +286,8 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WP
         const bool more = i <= ie;
         const unsigned nb = more ? pbytes : 0u;
         const int d2 = more ? 2 : 0, d1 = more ? 1 : 0;
-        const auto rA2 = plane_rsrc(p.A + (i64(i + d2) * si - p.poff), nb);
-        const auto rB1 = plane_rsrc(p.B + (i64(i + d1) * si - p.poff), nb);
+        const auto rA2 = prs(p.A, i + d2, nb);
+        const auto rB1 = prs(p.B, i + d1, nb);
 #pragma unroll
         for (int r = 0; r < R; ++r) {
             a[S3][r] = bld<T>(rA2, oa[r]);
@@ -258,13 +320,13 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WP
 #pragma unroll
         for (int r = 0; r < R; ++r) xnA[r] = a[S2][r], xpA[r] = a[S0][r];
         if (ALIAS && i == p.an_i) {
-            const auto rs = plane_rsrc(p.an - p.poff, pbytes);
+            const auto rs = plane_rsrc(p.an, pbytes);
 #pragma unroll
             for (int r = 0; r < R; ++r) xnA[r] = bld<T>(rs, oa[r]);
             rxn = bld<T>(rs, ra_off);
         }
         if (ALIAS && i == p.ap_i) {
-            const auto rs = plane_rsrc(p.ap - p.poff, pbytes);
+            const auto rs = plane_rsrc(p.ap, pbytes);
 #pragma unroll
             for (int r = 0; r < R; ++r) xpA[r] = bld<T>(rs, oa[r]);
             rxp = bld<T>(rs, ra_off);
@@ -302,37 +364,27 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WP
         }
 
         // own C(i): store, wrap, error (only the work item's own planes)
-        if (i >= ib && i <= ie) {
-            const auto rc = prs(p.C, i);
+        if (own(i)) {
+            if constexpr (!DELTA) {
+                const auto rc = prs(p.C, i, pbytes);
 #pragma unroll
-            for (int r = 0; r < R; ++r)
-                if constexpr (!DELTA) bst<kStAux>(c[S0][r], rc, os[r]);
+                for (int r = 0; r < R; ++r) bst<kStAux>(c[S0][r], rc, os[r]);
+                if (rare & 3) {
 #pragma unroll
-            for (int g = 0; g < 2; ++g)
-                if (!DELTA && i >= p.wc_lo[g] && i <= p.wc_hi[g]) {
-                    const auto rw = prs(p.C, i + p.wc_sh[g]);
+                    for (int g = 0; g < 2; ++g)
+                        if (i >= p.wc_lo[g] && i <= p.wc_hi[g]) {
+                            const auto rw = prs(p.C, i + p.wc_sh[g], pbytes);
 #pragma unroll
-                    for (int r = 0; r < R; ++r) bst<kStAux>(c[S0][r], rw, os[r]);
+                            for (int r = 0; r < R; ++r) bst<kStAux>(c[S0][r], rw, os[r]);
+                        }
                 }
-            const bool erow = i >= p.ei0 && i <= p.ei1;
-            const T sx = ldconst(p.tx, i);
-#pragma unroll
-            for (int r = 0; r < R; ++r) {
-                if (!ovalid[r]) continue;
-                if constexpr (ABL == 1) continue;
-                chk1 += c[S0][r];
-                if constexpr (ABL == 2) {
-                    if (erow) {
-                        const T e = absval(c[S0][r] - analytic(sx, oty[r], otz, p.ctC));
-                        if (e > ma1) ma1 = e;
-                    }
-                } else if (erow) accumulate_error_dev(c[S0][r], analytic(sx, oty[r], otz, p.ctC), ma1, mr1);
             }
+            errors(c[S0], i, p.ctC, ma1, mr1, chk1);
         }
 
         // D(i-1) from the C(i-1) tile (written last iteration, other buffer)
         const int id = i - 1;
-        if (id >= ib && id <= ie) {
+        if (own(id)) {
             T dv[R];
 #pragma unroll
             for (int r = 0; r < R; ++r) {
@@ -348,42 +400,33 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WP
                     dv[r] = leapfrog(c[S3][r], a[S0][r], lap, p.coefD);
                 }
             }
-            const auto rd = prs(p.D, id);
+            const auto rd = prs(p.D, id, pbytes);
 #pragma unroll
             for (int r = 0; r < R; ++r) bst<kStAux>(dv[r], rd, os[r]);
             if constexpr (DELTA) {
-                const auto rdc = prs(p.C, id);
+                const auto rdc = prs(p.C, id, pbytes);
 #pragma unroll
                 for (int r = 0; r < R; ++r) bst<kStAux>(dl[H1][r], rdc, os[r]);
+                if (rare & 3) {
+#pragma unroll
+                    for (int g = 0; g < 2; ++g)
+                        if (id >= p.wc_lo[g] && id <= p.wc_hi[g]) {
+                            const auto rw = prs(p.C, id + p.wc_sh[g], pbytes);
+#pragma unroll
+                            for (int r = 0; r < R; ++r) bst<kStAux>(dl[H1][r], rw, os[r]);
+                        }
+                }
+            }
+            if (rare & 12) {
 #pragma unroll
                 for (int g = 0; g < 2; ++g)
-                    if (id >= p.wc_lo[g] && id <= p.wc_hi[g]) {
-                        const auto rw = prs(p.C, id + p.wc_sh[g]);
+                    if (id >= p.wd_lo[g] && id <= p.wd_hi[g]) {
+                        const auto rw = prs(p.D, id + p.wd_sh[g], pbytes);
 #pragma unroll
-                        for (int r = 0; r < R; ++r) bst<kStAux>(dl[H1][r], rw, os[r]);
+                        for (int r = 0; r < R; ++r) bst<kStAux>(dv[r], rw, os[r]);
                     }
             }
-#pragma unroll
-            for (int g = 0; g < 2; ++g)
-                if (id >= p.wd_lo[g] && id <= p.wd_hi[g]) {
-                    const auto rw = prs(p.D, id + p.wd_sh[g]);
-#pragma unroll
-                    for (int r = 0; r < R; ++r) bst<kStAux>(dv[r], rw, os[r]);
-                }
-            const bool erow = id >= p.ei0 && id <= p.ei1;
-            const T sx = ldconst(p.tx, id);
-#pragma unroll
-            for (int r = 0; r < R; ++r) {
-                if (!ovalid[r]) continue;
-                if constexpr (ABL == 1) continue;
-                chk2 += dv[r];
-                if constexpr (ABL == 2) {
-                    if (erow) {
-                        const T e = absval(dv[r] - analytic(sx, oty[r], otz, p.ctD));
-                        if (e > ma2) ma2 = e;
-                    }
-                } else if (erow) accumulate_error_dev(dv[r], analytic(sx, oty[r], otz, p.ctD), ma2, mr2);
-            }
+            errors(dv, id, p.ctD, ma2, mr2, chk2);
         }
     };
 
@@ -391,7 +434,7 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WP
         prefetch(phase, i);
         stage(phase);
         __syncthreads();
-        if (i == p.an_i || i == p.ap_i) compute(phase, std::true_type{}, i);
+        if ((rare & 16) && (i == p.an_i || i == p.ap_i)) compute(phase, std::true_type{}, i);
         else compute(phase, std::false_type{}, i);
     };
 
@@ -471,22 +514,29 @@ bool tb2_supported(int rows, int waves, int occ, int nwk) {
 template <class T>
 void launch_tb2(int rows, int waves, int occ, int nwk, bool delta, bool first, const T* A, const T* B, T* C, T* D, const GridView& gv,
                 const Box* boxes, int nbox, const Box& cdom, int ei0, int ei1, const Wrap& wrapC,
-                const Wrap& wrapD, const SeamAlias<T>& alias, const T* tx, const T* ty,
-                const T* tz, const StepCoefs& cC, const StepCoefs& cD, u64* errC, u64* errD,
+                const Wrap& wrapD, const SeamAlias<T>& alias, const T* txy, const T* tz,
+                const StepCoefs& cC, const StepCoefs& cD, u64* errC, u64* errD,
                 int chunk, hipStream_t s) {
     W3D_REQUIRE(gv.G >= 2, "temporal blocking needs ghost depth >= 2");
     W3D_REQUIRE(tb2_supported(rows, waves, occ, nwk), "tb2: unsupported rows x waves x occupancy x k-waves");
     W3D_REQUIRE(!delta || (occ == 0 && tb2_delta_supported(rows, waves, nwk)),
                 "tb2 increment form: tiles r2w4, r2w8, r4w4, r2w8k2 only");
     W3D_REQUIRE(nbox >= 1 && nbox <= kMaxBoxes, "bad box count");
+    W3D_REQUIRE(gv.si * i64(sizeof(T)) < (i64(1) << 31), "tb2: plane larger than 2 GiB");
     TbParams<T> p{};
     p.xcd = xcd_swizzle_enabled();
-    p.jfirst = tile_order_jfirst();
-    p.A = A;
-    p.B = B;
-    p.C = C;
-    p.D = D;
-    p.si = gv.si;
+    p.order = tile_order();
+    // plane indices reach 1 - G (wrap targets) and ib - 2 >= -1
+    p.pbytes = unsigned(gv.si * i64(sizeof(T)));
+    p.pbias = gv.G + 1;
+    auto biased = [&](const T* base) {
+        return reinterpret_cast<char*>(reinterpret_cast<uintptr_t>(base - gv.poff) -
+                                       uintptr_t(p.pbias) * p.pbytes);
+    };
+    p.A = biased(A);
+    p.B = biased(B);
+    p.C = biased(C);
+    p.D = biased(D);
     p.sj = gv.sj;
     p.poff = gv.poff;
     p.jmin = 1 - gv.G;
@@ -503,10 +553,10 @@ void launch_tb2(int rows, int waves, int occ, int nwk, bool delta, bool first, c
     wrap_ranges(wrapD, p.wd_lo, p.wd_hi, p.wd_sh);
     p.an_i = alias.next ? alias.next_i : INT_MIN;
     p.ap_i = alias.prev ? alias.prev_i : INT_MIN;
-    p.an = alias.next;
-    p.ap = alias.prev;
-    p.tx = tx;
-    p.ty = ty;
+    p.an = alias.next ? alias.next - gv.poff : nullptr;
+    p.ap = alias.prev ? alias.prev - gv.poff : nullptr;
+    p.txy = txy;
+    p.tpj = gv.Y + 2;
     p.tz = tz;
     p.hx2 = T(cC.hx2);
     p.hy2 = T(cC.hy2);
@@ -554,7 +604,7 @@ void launch_tb2(int rows, int waves, int occ, int nwk, bool delta, bool first, c
     template void launch_tb2<T>(int, int, int, int, bool, bool, const T*, const T*, T*, T*, const GridView&, \
                                 const Box*, int, const Box&, int, int, const Wrap&,          \
                                 const Wrap&, const SeamAlias<T>&, const T*, const T*,        \
-                                const T*, const StepCoefs&, const StepCoefs&, u64*, u64*,    \
+                                const StepCoefs&, const StepCoefs&, u64*, u64*,              \
                                 int, hipStream_t);
 W3D_TB_INST(double)
 W3D_TB_INST(float)
