@@ -484,10 +484,10 @@ int march_tile_rows(const KernelVariant& v) {
 int tile_order() {
     static const int order = [] {
         const char* e = std::getenv("WAVE3D_TILE_ORDER");
-        if (!e || !*e) return 1;
+        if (!e || !*e) return 2;
         if (e[0] == 'k') return 0;
-        if (e[0] == 'b') return 2;
-        return 1;
+        if (e[0] == 'j') return 1;
+        return 2;
     }();
     return order;
 }

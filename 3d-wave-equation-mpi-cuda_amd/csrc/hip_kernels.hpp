@@ -157,11 +157,11 @@ int march_tile_rows(const KernelVariant& v);
 // XCD-aware workgroup order for the stencil kernels (device_common.hpp xcd_swizzle);
 // opt-in via env WAVE3D_XCD_SWIZZLE=1 (ablation, not faster on MI355X).
 bool xcd_swizzle_enabled();
-// Temporal-blocking tile order (env WAVE3D_TILE_ORDER): 1 = "j" (default): j-neighbour tiles at
-// consecutive block ids, so k-neighbours are a multiple of 8 ids apart and share an XCD (their
-// halo lines then hit that XCD's L2: -17 % memory-side reads, profiles/tile_order_r2.txt);
-// 0 = "k": k-fastest; 2 = "band": XCD x (block id mod 8) owns a band of tiles_j/8 adjacent tile
-// rows for every k, so j-neighbours inside a band share its L2 as well.
+// Temporal-blocking tile order (env WAVE3D_TILE_ORDER): 2 = "band" (default): XCD x (block id
+// mod 8) owns a band of tiles_j/8 adjacent tile rows for every k-tile, so k-neighbours and the
+// j-neighbours inside a band share its L2 (-12 % memory-side reads vs "j", -30 % vs "k";
+// profiles/tile_order_r2.txt; needs tiles_j % 8 == 0, else "j"); 1 = "j": j-neighbour tiles at
+// consecutive block ids (k-neighbours a multiple of 8 ids apart, same XCD); 0 = "k": k-fastest.
 int tile_order();
 
 // Temporal blocking: one sweep computes layers m (C) and m+1 (D) from A = u^{m-1} and
