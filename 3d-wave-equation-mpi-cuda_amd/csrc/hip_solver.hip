@@ -1323,6 +1323,9 @@ private:
                     if (wp.src[q] >= 1) copy_plane(R, lp, wp.src[q], wp.dst[q]);
             }
         }
+        // device-to-device hipMemcpy need not block the host, and the sweeps run on
+        // non-blocking streams: the restored levels must be complete before the first one
+        HIP_CHECK(hipDeviceSynchronize());
         if (tb_ && tb_halo(ranks_[0])) {
             exchange_tb(n, s_comp_);  // A level = u^n (2 deep + alias), B level = u^{n-1}
         } else {
