@@ -184,6 +184,21 @@ inline int auto_chunk(int best, int planes, int tiles) {
     return std::min(std::max(1, c), planes);
 }
 
+// The same decision for one launch over several boxes (tiles[q] x planes[q] each), taken for
+// the launch as a whole: decided per box, the thin overlap shells (a few tiles each) got 8-16-
+// plane work items whose 2-plane prologues were 12-25 % redundant work, while the launch had
+// plenty of workgroups. Returns the chunk before clamping to each box's planes.
+inline int auto_chunk_boxes(int best, const int* tiles, const int* planes, int n) {
+    constexpr int kTarget = 4 * 256;
+    i64 items = 0, work = 0;
+    for (int q = 0; q < n; ++q) {
+        items += i64(tiles[q]) * cdiv(planes[q], best);
+        work += i64(tiles[q]) * planes[q];
+    }
+    if (items >= kTarget) return best;
+    return std::max(1, std::max(8, int(work / kTarget)));
+}
+
 // ---- buffer addressing (T8): wave-uniform plane descriptor + 32-bit lane byte offset -----
 // An offset >= the descriptor's byte size is out of range: loads return 0, stores are
 // dropped — masked lanes use kOOB instead of a branch around the access.

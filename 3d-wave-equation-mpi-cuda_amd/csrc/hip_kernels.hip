@@ -627,6 +627,16 @@ void launch_step(const KernelVariant& kind, bool first, const T* u1, const T* u2
         HIP_OK(hipGetLastError());
         return;
     }
+    int btiles[kMaxBoxes], bplanes[kMaxBoxes], nbt = 0;
+    for (int q = 0; q < nbox; ++q) {
+        const Box& bx = boxes[q];
+        if (bx.empty()) continue;
+        btiles[nbt] = ((bx.k1 - 1) / kTK - (bx.k0 - 1) / kTK + 1) * cdiv(bx.j1 - bx.j0 + 1, tj_rows);
+        bplanes[nbt++] = bx.i1 - bx.i0 + 1;
+    }
+    // 32-plane work items (chunk sweep on MI355X, profiles/), shorter on small grids so that
+    // there are enough workgroups to fill the 256 CUs
+    const int achunk = auto_chunk_boxes(32, btiles, bplanes, nbt);
     for (int q = 0; q < nbox; ++q) {
         const Box& bx = boxes[q];
         if (bx.empty()) continue;
@@ -640,17 +650,8 @@ void launch_step(const KernelVariant& kind, bool first, const T* u1, const T* u2
         L.tiles_k = t1 - t0 + 1;
         L.tiles_j = cdiv(bx.j1 - bx.j0 + 1, tj_rows);
         const int planes = bx.i1 - bx.i0 + 1;
-        int ch = 1;
-        {
-            if (chunk > 0) {
-                ch = std::min(chunk, planes);
-            } else {
-                // 32-plane work items (chunk sweep on MI355X, profiles/), shorter on small
-                // grids so that there are enough workgroups to fill the 256 CUs
-                ch = auto_chunk(32, planes, L.tiles_k * L.tiles_j);
-            }
-            ch = cdiv(planes, cdiv(planes, ch));  // equal work items (no short tail chunk)
-        }
+        int ch = std::min(chunk > 0 ? chunk : achunk, planes);
+        ch = cdiv(planes, cdiv(planes, ch));  // equal work items (no short tail chunk)
         L.chunk = ch;
         L.block_begin = total;
         total += L.tiles_k * L.tiles_j * cdiv(planes, ch);

@@ -571,6 +571,14 @@ void launch_tb2(int rows, int waves, int occ, int nwk, bool delta, bool first, c
     p.errC = errC;
     p.errD = errD;
     const int TJ = waves / nwk * rows, TK = kTK * nwk;
+    int btiles[kMaxBoxes], bplanes[kMaxBoxes], nbt = 0;
+    for (int q = 0; q < nbox; ++q) {
+        const Box& bx = boxes[q];
+        if (bx.empty()) continue;
+        btiles[nbt] = ((bx.k1 - 1) / TK - (bx.k0 - 1) / TK + 1) * cdiv(bx.j1 - bx.j0 + 1, TJ) * nwk;
+        bplanes[nbt++] = bx.i1 - bx.i0 + 1;
+    }
+    const int achunk = auto_chunk_boxes(96, btiles, bplanes, nbt);
     int nb = 0, total = 0;
     for (int q = 0; q < nbox; ++q) {
         const Box& bx = boxes[q];
@@ -585,8 +593,7 @@ void launch_tb2(int rows, int waves, int occ, int nwk, bool delta, bool first, c
         L.tiles_k = t1 - t0 + 1;
         L.tiles_j = cdiv(bx.j1 - bx.j0 + 1, TJ);
         const int planes = bx.i1 - bx.i0 + 1;
-        const int want = chunk > 0 ? std::min(chunk, planes)
-                                   : auto_chunk(96, planes, L.tiles_k * L.tiles_j * nwk);
+        const int want = std::min(chunk > 0 ? chunk : achunk, planes);
         L.chunk = cdiv(planes, cdiv(planes, want));  // equal work items (no short tail chunk)
         L.block_begin = total;
         total += L.tiles_k * L.tiles_j * cdiv(planes, L.chunk);
