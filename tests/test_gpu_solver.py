@@ -351,3 +351,25 @@ def test_delta_scheme_checkpoint_resume(C, tmp_path, ranks, dims):
 
     assert diff(full) == [], f"uninterrupted run vs oracle, layers {diff(full)}"
     assert diff(res) == [], f"resumed run vs oracle, layers {diff(res)}"
+
+
+@pytest.mark.parametrize("kernel", ["tb2r2w8", "tb2r2w8k2"])
+def test_tile_orders_bitwise(C, kernel):
+    """The XCD-band (default), j-fastest and k-fastest tile orders of the temporal-blocking
+    sweep give the same per-layer error maxima, bit for bit (N=129: 8 tile rows, so the band
+    order is active). The order is read once per process (WAVE3D_TILE_ORDER): one subprocess
+    each."""
+    import json
+    import sys
+
+    code = ("import json, wave3d; r = wave3d.WaveSolver(wave3d.WaveProblem(129, timesteps=20), "
+            f"'hip', kernel='{kernel}').run(); print(json.dumps([r.max_abs, r.max_rel]))")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = {}
+    for order in ("band", "j", "k"):
+        env = dict(os.environ, WAVE3D_TILE_ORDER=order)
+        p = subprocess.run([sys.executable, "-c", code], cwd=root, env=env, capture_output=True,
+                           text=True, timeout=120)
+        assert p.returncode == 0, p.stderr[-2000:]
+        out[order] = json.loads(p.stdout.strip().splitlines()[-1])
+    assert out["band"] == out["j"] == out["k"]
