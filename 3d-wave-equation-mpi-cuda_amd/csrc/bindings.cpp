@@ -233,10 +233,23 @@ void k_tb3_dense(int rows, int waves, bool first, uintptr_t A, uintptr_t B, uint
     W3D_REQUIRE(v.G >= 3, "k_tb3 needs ghost depth >= 3");
     std::vector<Box> bx;
     for (auto& b : boxes) bx.push_back(tobox(b));
-    launch_tb3<T>(rows, waves, first, P<T>(A) + o, P<T>(B) + o, P<T>(D) + o, P<T>(E) + o, v,
-                  bx.data(), int(bx.size()), tobox(cdom), ei0, ei1, Wrap{}, Wrap{},
-                  SeamPartners<T>{}, P<T>(tx), P<T>(ty), P<T>(tz), tocoefs(cC), tocoefs(cD),
-                  tocoefs(cE), P<u64>(errC), P<u64>(errD), P<u64>(errE), chunk, (hipStream_t)stream);
+    const hipStream_t s = (hipStream_t)stream;
+    T* txy = nullptr;
+    if (hipMalloc(&txy, txy_elems(v.X, v.Y) * sizeof(T)) != hipSuccess) throw Error("k_tb3: hipMalloc failed");
+    try {
+        launch_txy<T>(txy, P<T>(tx), P<T>(ty), v.X, v.Y, s);
+        launch_tb3<T>(rows, waves, first, P<T>(A) + o, P<T>(B) + o, P<T>(D) + o, P<T>(E) + o, v,
+                      bx.data(), int(bx.size()), tobox(cdom), ei0, ei1, Wrap{}, Wrap{},
+                      SeamPartners<T>{}, txy, P<T>(tz), tocoefs(cC), tocoefs(cD),
+                      tocoefs(cE), P<u64>(errC), P<u64>(errD), P<u64>(errE), chunk, s);
+    } catch (...) {
+        (void)hipStreamSynchronize(s);
+        (void)hipFree(txy);
+        throw;
+    }
+    const hipError_t e = hipStreamSynchronize(s);
+    (void)hipFree(txy);
+    if (e != hipSuccess) throw Error(std::string("k_tb3: ") + hipGetErrorString(e));
 }
 
 template <class T>

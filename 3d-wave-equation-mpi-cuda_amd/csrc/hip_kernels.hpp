@@ -124,8 +124,8 @@ bool tb3_supported(int rows, int waves);
 template <class T>
 void launch_tb3(int rows, int waves, bool first, const T* A, const T* B, T* D, T* E,
                 const GridView& gv, const Box* boxes, int nbox, const Box& cdom, int ei0, int ei1,
-                const Wrap& wrapD, const Wrap& wrapE, const SeamPartners<T>& seam, const T* tx,
-                const T* ty, const T* tz, const StepCoefs& cC, const StepCoefs& cD,
+                const Wrap& wrapD, const Wrap& wrapE, const SeamPartners<T>& seam, const T* txy,
+                const T* tz, const StepCoefs& cC, const StepCoefs& cD,
                 const StepCoefs& cE, u64* errC, u64* errD, u64* errE, int chunk, hipStream_t s);
 
 // Box halo staging for the temporal-blocking exchange on y/z splits: copy the logical box

@@ -733,7 +733,10 @@ private:
             al.prev = R.alias_buf + R.plane_off;
         }
         if (!boxes) boxes = &R.compute, nbox = 1;
-        launch_tb2<T>(tb_rows_, tb_waves_, tb_occ_, tb_nwk_, cfg_.delta, m == 1, A, B, R.g[lvl(m)], R.g[lvl(m + 1)], R.gv, boxes, nbox,
+        // two-layer tails of a tb3 run whose tile has no tb2 instantiation (1-row tiles) use
+        // the default tb2 tile
+        const bool own = tb2_supported(tb_rows_, tb_waves_, tb_occ_, tb_nwk_);
+        launch_tb2<T>(own ? tb_rows_ : 2, own ? tb_waves_ : 8, own ? tb_occ_ : 0, own ? tb_nwk_ : 1, cfg_.delta, m == 1, A, B, R.g[lvl(m)], R.g[lvl(m + 1)], R.gv, boxes, nbox,
                       R.cdom, R.error.i0, R.error.i1, R.wrap, R.wrap2, al, R.txy, R.tz,
                       coefs(m), coefs(m + 1), R.err + size_t(m) * kSlotsPerLayer,
                       R.err + size_t(m + 1) * kSlotsPerLayer, cfg_.chunk, s);
@@ -785,7 +788,7 @@ private:
         const SeamPartners<T> sp = seam_partners(R, m, nullptr);
         if (!boxes) boxes = &R.compute, nbox = 1;
         launch_tb3<T>(tb_rows_, tb_waves_, m == 1, A, B, R.g[lvl(m + 1)], R.g[lvl(m + 2)], R.gv, boxes,
-                      nbox, R.cdom, R.error.i0, R.error.i1, R.wrap2, R.wrap3, sp, R.tx, R.ty, R.tz,
+                      nbox, R.cdom, R.error.i0, R.error.i1, R.wrap2, R.wrap3, sp, R.txy, R.tz,
                       coefs(m), coefs(m + 1), coefs(m + 2), R.err + size_t(m) * kSlotsPerLayer,
                       R.err + size_t(m + 1) * kSlotsPerLayer, R.err + size_t(m + 2) * kSlotsPerLayer,
                       cfg_.chunk, s);

@@ -35,11 +35,15 @@ namespace {
 
 template <class T>
 struct Tb3Params {
-    const T* A;
-    const T* B;
-    T* D;
-    T* E;
-    i64 si;
+    // level bases pre-biased on the host (as in k_tb2): plane i's block starts at
+    // base + (i + pbias) * pbytes, one 32x32->64-bit product per descriptor
+    const char* A;
+    const char* B;
+    char* D;
+    char* E;
+    unsigned pbytes;
+    int pbias;
+    int order;  // tile order (tile_order(): 0 k-fastest, 1 j-fastest, 2 XCD bands; as k_tb2)
     int sj;
     int poff;
     int jmin, jmax, kmin, kmax;  // storage bounds (logical)
@@ -53,8 +57,9 @@ struct Tb3Params {
     // the x+ neighbour of D is nC (C at the partner plane); mirrored for ap_i / x-.
     int an_i, ap_i;
     const T *nA, *nC, *pA, *pC;
-    const T* tx;
-    const T* ty;
+    // txy[i * tpj + j] = RN(tx[i] * ty[j]) (launch_txy): f = (txy * sz) * ct, two multiplies
+    const T* txy;
+    int tpj;
     const T* tz;
     T hx2, hy2, hz2, yx2, yy2, yz2;
     T coefC, coefD, coefE, ctC, ctD, ctE;
@@ -63,16 +68,24 @@ struct Tb3Params {
     u64* errE;
 };
 
-template <class T, bool FIRST, int R, int NW>
-__global__ void __launch_bounds__(NW * 64) k_tb3(const Tb3Params<T> p) {
+// Ring ownership: each ring node belongs to ONE thread (threads [0, N1) the 1-ring, then the
+// 2-ring, then the 3-ring without its corners, which no in-plane 5-point stencil reads), RP
+// positions per thread when the rings outnumber the threads. A thread keeps four A slots, two B
+// slots and (1-ring) four C slots per position — 10 values instead of the 18 a thread held when
+// every thread owned one node of each ring (round 1), which put the fp64 kernel at 191-256 VGPRs.
+// WPE: minimum waves per SIMD the register allocation must allow (1-row tiles: 4, i.e. two
+// 8-wave or one 16-wave workgroup per CU).
+template <class T, bool FIRST, int R, int NW, int WPE = (R == 1 ? 4 : 1)>
+__global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WPE, 8))) k_tb3(const Tb3Params<T> p) {
     constexpr int TJ = NW * R;
     constexpr int AH = TJ + 6, AW = kTK + 6;  // A tile origin (jt-3, kb-3)
     constexpr int CH = TJ + 4, CW = kTK + 4;  // C tile origin (jt-2, kb-2)
     constexpr int DH = TJ + 2, DW = kTK + 2;  // D tile origin (jt-1, kb-1)
     constexpr int N1 = 2 * kTK + 2 * (TJ + 2);        // 1-ring positions
     constexpr int N2 = 2 * (kTK + 2) + 2 * (TJ + 4);  // 2-ring positions
-    constexpr int N3 = 2 * (kTK + 4) + 2 * (TJ + 6);  // 3-ring positions (A only)
-    static_assert(N1 <= NW * 64 && N2 <= NW * 64 && N3 <= NW * 64, "rings need more lanes");
+    constexpr int N3 = 2 * (kTK + 4) + 2 * (TJ + 4);  // 3-ring positions (A only, no corners)
+    constexpr int NT = NW * 64;
+    constexpr int RP = (N1 + N2 + N3 + NT - 1) / NT;  // ring positions per thread
     constexpr unsigned ES = sizeof(T);
     __shared__ T ldsA[2][AH][AW];
     __shared__ T ldsC[2][CH][CW];
@@ -82,32 +95,49 @@ __global__ void __launch_bounds__(NW * 64) k_tb3(const Tb3Params<T> p) {
     const int b = find_box(p, bid);
     const BoxLaunch Bx = p.box[b];
     int local = bid - Bx.block_begin;
-    const int tk = local % Bx.tiles_k;
-    local /= Bx.tiles_k;
-    const int tj = local % Bx.tiles_j;
-    const int ci = local / Bx.tiles_j;
+    int tk, tj;
+    if (p.order == 2 && Bx.tiles_j % kXcds == 0) {
+        // XCD x = id mod 8 runs tile rows [x*hb, x*hb + hb) of every k-tile and chunk
+        const int hb = Bx.tiles_j / kXcds, x = local % kXcds;
+        local /= kXcds;
+        tj = x * hb + local % hb;
+        local /= hb;
+        tk = local % Bx.tiles_k;
+        local /= Bx.tiles_k;
+    } else if (p.order) {
+        tj = local % Bx.tiles_j;
+        local /= Bx.tiles_j;
+        tk = local % Bx.tiles_k;
+        local /= Bx.tiles_k;
+    } else {
+        tk = local % Bx.tiles_k;
+        local /= Bx.tiles_k;
+        tj = local % Bx.tiles_j;
+        local /= Bx.tiles_j;
+    }
+    const int ci = local;
     const int kb = Bx.kbase + tk * kTK;
     const int jt = Bx.j0 + tj * TJ;
     const int ib = Bx.i0 + ci * Bx.chunk;
     const int ie = min(Bx.i1, ib + Bx.chunk - 1);
     const int lane = threadIdx.x & 63;
-    const int q = threadIdx.x;
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const i64 si = p.si;
     const int sj = p.sj;
-    const unsigned pbytes = unsigned(si) * ES;
+    const unsigned pbytes = p.pbytes;
 
     auto inb = [&](int j, int k) { return j >= p.jmin && j <= p.jmax && k >= p.kmin && k <= p.kmax; };
     auto incd = [&](int j, int k) { return j >= p.cj0 && j <= p.cj1 && k >= p.ck0 && k <= p.ck1; };
     auto boff = [&](int j, int k, bool ok) { return ok ? unsigned(j * sj + k + p.poff) * ES : kOOB; };
-    auto prs = [&](const T* base, int i) { return plane_rsrc(base + (i64(i) * si - p.poff), pbytes); };
+    // descriptor of logical plane i of a level (`nb` bytes: 0 = loads return 0)
+    auto prs = [&](const char* base, int i, unsigned nb) {
+        return plane_rsrc(base + u64(unsigned(i + p.pbias)) * pbytes, nb);
+    };
     auto lrs = [&](const T* plane) { return plane_rsrc(plane - p.poff, pbytes); };
 
     // ---- own nodes ------------------------------------------------------------------------
     const int k = kb + lane;
     unsigned oa[R], ob[R], os[R];
     bool ovalid[R], ocd[R];
-    T oty[R];
 #pragma unroll
     for (int r = 0; r < R; ++r) {
         const int j = jt + w * R + r;
@@ -116,45 +146,56 @@ __global__ void __launch_bounds__(NW * 64) k_tb3(const Tb3Params<T> p) {
         oa[r] = boff(j, k, inb(j, k));
         ob[r] = boff(j, k, !FIRST && inb(j, k) && ocd[r]);
         os[r] = boff(j, k, ovalid[r]);
-        oty[r] = ldconst(p.ty, min(j, Bx.j1));  // wave-uniform row: a scalar load, SGPRs
     }
     const T otz = (k >= Bx.k0 && k <= Bx.k1) ? p.tz[k] : T(0);
+    // rows of this wave in the sx*sy table (padded past the last row: masked rows read in bounds)
+    const T* const txw = p.txy + (jt + w * R);
+    // self-wrap ranges of D / E met by this work item (wave-uniform bits, one test per plane)
+    int rare = 0;
+#pragma unroll
+    for (int g = 0; g < 2; ++g) {
+        if (p.wd_lo[g] <= ie && p.wd_hi[g] >= ib) rare |= 1;
+        if (p.we_lo[g] <= ie && p.we_hi[g] >= ib) rare |= 2;
+    }
+    rare = __builtin_amdgcn_readfirstlane(rare);
 
-    // ---- ring positions: d-ring = rows jt-d / jt+TJ-1+d over cols kb-d+1 .. kb+64+d-2, then
-    //      cols kb-d / kb+63+d over rows jt-d .. jt+TJ-1+d -------------------------------------
-    auto ring = [&](int d, int idx, int& rj, int& rk) {
-        const int wd = kTK + 2 * (d - 1), hd = TJ + 2 * d;
+    // ---- ring positions of this thread ------------------------------------------------------
+    // d-ring = rows jt-d / jt+TJ-1+d over cols kb-d+1 .. kb+64+d-2, then cols kb-d / kb+63+d over
+    // rows jt-d+c .. jt+TJ-1+d-c (c = 1 drops the corners)
+    auto ring = [&](int d, int c, int idx, int& rj, int& rk) {
+        const int wd = kTK + 2 * (d - 1), hd = TJ + 2 * (d - c);
         if (idx < wd) rj = jt - d, rk = kb - (d - 1) + idx;
         else if (idx < 2 * wd) rj = jt + TJ - 1 + d, rk = kb - (d - 1) + idx - wd;
-        else if (idx < 2 * wd + hd) rj = jt - d + (idx - 2 * wd), rk = kb - d;
-        else rj = jt - d + (idx - 2 * wd - hd), rk = kb + kTK - 1 + d;
+        else if (idx < 2 * wd + hd) rj = jt - d + c + (idx - 2 * wd), rk = kb - d;
+        else rj = jt - d + c + (idx - 2 * wd - hd), rk = kb + kTK - 1 + d;
     };
-    int r1j = 0, r1k = 0, r2j = 0, r2k = 0, r3j = 0, r3k = 0;
-    const bool on1 = q < N1, on2 = q < N2, on3 = q < N3;
-    if (on1) ring(1, q, r1j, r1k);
-    if (on2) ring(2, q, r2j, r2k);
-    if (on3) ring(3, q, r3j, r3k);
-    const bool cd1 = on1 && incd(r1j, r1k), cd2 = on2 && incd(r2j, r2k);
-    const unsigned r1a = boff(r1j, r1k, on1 && inb(r1j, r1k));
-    const unsigned r1b = boff(r1j, r1k, !FIRST && on1 && inb(r1j, r1k) && cd1);
-    const unsigned r2a = boff(r2j, r2k, on2 && inb(r2j, r2k));
-    const unsigned r2b = boff(r2j, r2k, !FIRST && on2 && inb(r2j, r2k) && cd2);
-    const unsigned r3a = boff(r3j, r3k, on3 && inb(r3j, r3k));
-    // LDS coordinates (A tile) of the rings
-    const int a1y = r1j - jt + 3, a1x = r1k - kb + 3;
-    const int a2y = r2j - jt + 3, a2x = r2k - kb + 3;
-    const int a3y = r3j - jt + 3, a3x = r3k - kb + 3;
+    int rg[RP], ry[RP], rx[RP];      // ring (0: none) and A-tile coordinates
+    unsigned ra_off[RP], rb_off[RP];  // A / B load offsets (kOOB when masked)
+    bool rcd[RP];                     // stencil-valued node (else 0: Dirichlet face)
+#pragma unroll
+    for (int s = 0; s < RP; ++s) {
+        const int q = threadIdx.x + s * NT;
+        int g = 0, rj = jt, rk = kb;
+        if (q < N1) g = 1, ring(1, 0, q, rj, rk);
+        else if (q < N1 + N2) g = 2, ring(2, 0, q - N1, rj, rk);
+        else if (q < N1 + N2 + N3) g = 3, ring(3, 1, q - N1 - N2, rj, rk);
+        rg[s] = g;
+        ry[s] = rj - jt + 3, rx[s] = rk - kb + 3;
+        rcd[s] = g != 0 && g != 3 && incd(rj, rk);
+        ra_off[s] = boff(rj, rk, g != 0 && inb(rj, rk));
+        rb_off[s] = boff(rj, rk, !FIRST && rcd[s] && inb(rj, rk));
+    }
 
     // slots (iteration i = ib - 2 + q, phase P = q & 3):
     //   A(x), ring A(x): (x - ib + 3) & 3  -> A(i-1) = P, A(i) = P+1, A(i+1) = P+2, A(i+2) = P+3
-    //   C(x): (x - ib + 2) & 3             -> C(i) = P, C(i-1) = P+3, C(i-2) = P+2
+    //   C(x), ring C(x): (x - ib + 2) & 3  -> C(i) = P, C(i-1) = P+3, C(i-2) = P+2
     //   D(x): (x - ib + 3) & 3             -> D(i-1) = P, D(i-2) = P+3, D(i-3) = P+2
-    //   B(x), 3-ring A(x), LDS buffers: (x - ib + 2) & 1
+    //   B(x), ring B(x), LDS buffers: (x - ib + 2) & 1
     T a[4][R], c[4][R], d[4][R], bb[2][R];
-    T a1[4], c1[4], b1[2], a2[4], b2[2], a3[2];
+    T ra[RP][4], rb[RP][2], rc[RP][4];
     {
-        const auto r0 = prs(p.A, ib - 3), rA1 = prs(p.A, ib - 2), rA2 = prs(p.A, ib - 1);
-        const auto rB = prs(p.B, ib - 2);
+        const auto r0 = prs(p.A, ib - 3, pbytes), rA1 = prs(p.A, ib - 2, pbytes), rA2 = prs(p.A, ib - 1, pbytes);
+        const auto rB = prs(p.B, ib - 2, pbytes);
 #pragma unroll
         for (int r = 0; r < R; ++r) {
             a[0][r] = bld<T>(r0, oa[r]);
@@ -166,13 +207,17 @@ __global__ void __launch_bounds__(NW * 64) k_tb3(const Tb3Params<T> p) {
 #pragma unroll
             for (int s = 0; s < 4; ++s) c[s][r] = d[s][r] = T(0);
         }
-        a1[0] = bld<T>(r0, r1a), a1[1] = bld<T>(rA1, r1a), a1[2] = bld<T>(rA2, r1a), a1[3] = T(0);
-        a2[0] = bld<T>(r0, r2a), a2[1] = bld<T>(rA1, r2a), a2[2] = bld<T>(rA2, r2a), a2[3] = T(0);
-        b1[0] = bld<T>(rB, r1b), b1[1] = T(0);
-        b2[0] = bld<T>(rB, r2b), b2[1] = T(0);
-        a3[0] = bld<T>(rA1, r3a), a3[1] = T(0);
 #pragma unroll
-        for (int s = 0; s < 4; ++s) c1[s] = T(0);
+        for (int s = 0; s < RP; ++s) {
+            ra[s][0] = bld<T>(r0, ra_off[s]);
+            ra[s][1] = bld<T>(rA1, ra_off[s]);
+            ra[s][2] = bld<T>(rA2, ra_off[s]);
+            ra[s][3] = T(0);
+            rb[s][0] = bld<T>(rB, rb_off[s]);
+            rb[s][1] = T(0);
+#pragma unroll
+            for (int t = 0; t < 4; ++t) rc[s][t] = T(0);
+        }
     }
 
     T ma1 = T(kErrInit), ma2 = T(kErrInit);
@@ -188,6 +233,24 @@ __global__ void __launch_bounds__(NW * 64) k_tb3(const Tb3Params<T> p) {
     auto cval = [&](T ctr, T bv, T lap) {
         return FIRST ? taylor_first(ctr, lap, p.coefC) : leapfrog(ctr, bv, lap, p.coefC);
     };
+    // errors and finiteness sum of the own nodes of plane i of a layer (values v[r]); the
+    // uniform error-plane test sits outside the per-lane row masks (a scalar branch)
+    auto errors = [&](const T(&v)[R], const int i, const T ct, T& ma, RelArg<T>& mr, T& chk) {
+        if (i >= p.ei0 && i <= p.ei1) {
+            const T* const trow = txw + i * p.tpj;
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                if (!ovalid[r]) continue;
+                chk += v[r];
+                const T f = (ldconst(trow, r) * otz) * ct;  // = ((sx*sy)*sz)*ct, stencil_math analytic
+                accumulate_error_dev(v[r], f, ma, mr);
+            }
+        } else {
+#pragma unroll
+            for (int r = 0; r < R; ++r)
+                if (ovalid[r]) chk += v[r];
+        }
+    };
 
     auto plane = [&](auto phase, auto alias, const int i) {
         constexpr int P = decltype(phase)::value;
@@ -195,66 +258,69 @@ __global__ void __launch_bounds__(NW * 64) k_tb3(const Tb3Params<T> p) {
         constexpr int S0 = P & 3, S1 = (P + 1) & 3, S2 = (P + 2) & 3, S3 = (P + 3) & 3;
         constexpr int H0 = P & 1, H1 = (P + 1) & 1;
 
-        // ---- prefetch A(i+2), 3-ring A(i+1), B(i+1) (0-record descriptors when done) ----
+        // ---- prefetch A(i+2), B(i+1) (own and ring; 0-record descriptors when done) --------
         {
             const bool more = i <= ie + 1;
             const unsigned nb = more ? pbytes : 0u;
             const int d2 = more ? 2 : 0, d1 = more ? 1 : 0;
-            const auto rA2 = plane_rsrc(p.A + (i64(i + d2) * si - p.poff), nb);
-            const auto rA1 = plane_rsrc(p.A + (i64(i + d1) * si - p.poff), nb);
-            const auto rB1 = plane_rsrc(p.B + (i64(i + d1) * si - p.poff), nb);
+            const auto rA2 = prs(p.A, i + d2, nb);
+            const auto rB1 = prs(p.B, i + d1, nb);
 #pragma unroll
             for (int r = 0; r < R; ++r) {
                 a[S3][r] = bld<T>(rA2, oa[r]);
                 bb[H1][r] = bld<T>(rB1, ob[r]);
             }
-            a1[S3] = bld<T>(rA2, r1a);
-            a2[S3] = bld<T>(rA2, r2a);
-            b1[H1] = bld<T>(rB1, r1b);
-            b2[H1] = bld<T>(rB1, r2b);
-            a3[H1] = bld<T>(rA1, r3a);
+#pragma unroll
+            for (int s = 0; s < RP; ++s) {
+                ra[s][S3] = bld<T>(rA2, ra_off[s]);
+                rb[s][H1] = bld<T>(rB1, rb_off[s]);
+            }
         }
         // ---- stage A(i) --------------------------------------------------------------------
 #pragma unroll
         for (int r = 0; r < R; ++r) ldsA[H0][3 + w * R + r][3 + lane] = a[S1][r];
-        if (on1) ldsA[H0][a1y][a1x] = a1[S1];
-        if (on2) ldsA[H0][a2y][a2x] = a2[S1];
-        if (on3) ldsA[H0][a3y][a3x] = a3[H0];
+#pragma unroll
+        for (int s = 0; s < RP; ++s)
+            if (rg[s]) ldsA[H0][ry[s]][rx[s]] = ra[s][S1];
         __syncthreads();
 
         // ---- seam partners (uniform branch, rare) -------------------------------------------
-        T xnA[R], xpA[R], xnA1 = a1[S2], xpA1 = a1[S0], xnA2 = a2[S2], xpA2 = a2[S0];
-        T cnx[R], cpx[R], cnx1 = c1[S0], cpx1 = c1[S2];
+        T xnA[R], xpA[R], cnx[R], cpx[R];
+        T rxn[RP], rxp[RP], rcn[RP], rcp[RP];
 #pragma unroll
         for (int r = 0; r < R; ++r) xnA[r] = a[S2][r], xpA[r] = a[S0][r], cnx[r] = c[S0][r], cpx[r] = c[S2][r];
+#pragma unroll
+        for (int s = 0; s < RP; ++s) rxn[s] = ra[s][S2], rxp[s] = ra[s][S0], rcn[s] = rc[s][S0], rcp[s] = rc[s][S2];
         if constexpr (ALIAS) {
             // C(i): A partner as x+ (i == an_i) or x- (i == ap_i) neighbour
             if (i == p.an_i) {
                 const auto rs = lrs(p.nA);
 #pragma unroll
                 for (int r = 0; r < R; ++r) xnA[r] = bld<T>(rs, oa[r]);
-                xnA1 = bld<T>(rs, r1a);
-                xnA2 = bld<T>(rs, r2a);
+#pragma unroll
+                for (int s = 0; s < RP; ++s) rxn[s] = bld<T>(rs, ra_off[s]);
             }
             if (i == p.ap_i) {
                 const auto rs = lrs(p.pA);
 #pragma unroll
                 for (int r = 0; r < R; ++r) xpA[r] = bld<T>(rs, oa[r]);
-                xpA1 = bld<T>(rs, r1a);
-                xpA2 = bld<T>(rs, r2a);
+#pragma unroll
+                for (int s = 0; s < RP; ++s) rxp[s] = bld<T>(rs, ra_off[s]);
             }
             // D(i-1): C at the partner plane (k_seam_c, before the sweep)
             if (i - 1 == p.an_i) {
                 const auto rs = lrs(p.nC);
 #pragma unroll
                 for (int r = 0; r < R; ++r) cnx[r] = bld<T>(rs, oa[r]);
-                cnx1 = bld<T>(rs, r1a);
+#pragma unroll
+                for (int s = 0; s < RP; ++s) rcn[s] = bld<T>(rs, ra_off[s]);
             }
             if (i - 1 == p.ap_i) {
                 const auto rs = lrs(p.pC);
 #pragma unroll
                 for (int r = 0; r < R; ++r) cpx[r] = bld<T>(rs, oa[r]);
-                cpx1 = bld<T>(rs, r1a);
+#pragma unroll
+                for (int s = 0; s < RP; ++s) rcp[s] = bld<T>(rs, ra_off[s]);
             }
         }
 
@@ -266,36 +332,31 @@ __global__ void __launch_bounds__(NW * 64) k_tb3(const Tb3Params<T> p) {
             c[S0][r] = ocd[r] ? cval(a[S1][r], bb[H0][r], lap) : T(0);
             ldsC[H0][y - 1][x - 1] = c[S0][r];
         }
-        if (on1) {
-            const T lap = lapA(H0, a1y, a1x, a1[S1], xpA1, xnA1);
-            c1[S0] = cd1 ? cval(a1[S1], b1[H0], lap) : T(0);
-            ldsC[H0][a1y - 1][a1x - 1] = c1[S0];
-        }
-        if (on2) {
-            const T lap = lapA(H0, a2y, a2x, a2[S1], xpA2, xnA2);
-            ldsC[H0][a2y - 1][a2x - 1] = cd2 ? cval(a2[S1], b2[H0], lap) : T(0);
+#pragma unroll
+        for (int s = 0; s < RP; ++s) {
+            if (rg[s] == 1 || rg[s] == 2) {
+                const T lap = lapA(H0, ry[s], rx[s], ra[s][S1], rxp[s], rxn[s]);
+                const T cv = rcd[s] ? cval(ra[s][S1], rb[s][H0], lap) : T(0);
+                rc[s][S0] = cv;
+                ldsC[H0][ry[s] - 1][rx[s] - 1] = cv;
+            }
         }
         // C errors (own planes)
         if (i >= ib && i <= ie) {
-            const bool erow = i >= p.ei0 && i <= p.ei1;
-            const T sx = ldconst(p.tx, i);
-#pragma unroll
-            for (int r = 0; r < R; ++r) {
-                if (!ovalid[r]) continue;
-                chk1 += c[S0][r];
-                if (erow) accumulate_error_dev(c[S0][r], analytic(sx, oty[r], otz, p.ctC), ma1, mr1);
-            }
+            errors(c[S0], i, p.ctC, ma1, mr1, chk1);
         }
         if constexpr (!ALIAS) {
             // the x neighbours of D(i-1) are C(i) (computed just now) and C(i-2)
 #pragma unroll
             for (int r = 0; r < R; ++r) cnx[r] = c[S0][r];
-            cnx1 = c1[S0];
+#pragma unroll
+            for (int s = 0; s < RP; ++s) rcn[s] = rc[s][S0];
         } else {
             if (i - 1 != p.an_i) {
 #pragma unroll
                 for (int r = 0; r < R; ++r) cnx[r] = c[S0][r];
-                cnx1 = c1[S0];
+#pragma unroll
+                for (int s = 0; s < RP; ++s) rcn[s] = rc[s][S0];
             }
         }
 
@@ -311,32 +372,30 @@ __global__ void __launch_bounds__(NW * 64) k_tb3(const Tb3Params<T> p) {
                 d[S0][r] = ocd[r] ? leapfrog(c[S3][r], a[S0][r], lap, p.coefD) : T(0);
                 ldsD[H0][y - 1][x - 1] = d[S0][r];
             }
-            if (on1) {
-                const int y = a1y - 1, x = a1x - 1;
-                const T lap = laplace7_cr(c1[S3], cpx1, cnx1, ldsC[H1][y - 1][x], ldsC[H1][y + 1][x],
-                                          ldsC[H1][y][x - 1], ldsC[H1][y][x + 1], p.hx2, p.hy2,
-                                          p.hz2, p.yx2, p.yy2, p.yz2);
-                ldsD[H0][y - 1][x - 1] = cd1 ? leapfrog(c1[S3], a1[S0], lap, p.coefD) : T(0);
+#pragma unroll
+            for (int s = 0; s < RP; ++s) {
+                if (rg[s] == 1) {
+                    const int y = ry[s] - 1, x = rx[s] - 1;
+                    const T lap = laplace7_cr(rc[s][S3], rcp[s], rcn[s], ldsC[H1][y - 1][x],
+                                              ldsC[H1][y + 1][x], ldsC[H1][y][x - 1], ldsC[H1][y][x + 1],
+                                              p.hx2, p.hy2, p.hz2, p.yx2, p.yy2, p.yz2);
+                    ldsD[H0][y - 1][x - 1] = rcd[s] ? leapfrog(rc[s][S3], ra[s][S0], lap, p.coefD) : T(0);
+                }
             }
             if (id >= ib && id <= ie) {
-                const auto rd = prs(p.D, id);
+                const auto rd = prs(p.D, id, pbytes);
 #pragma unroll
                 for (int r = 0; r < R; ++r) bst<2>(d[S0][r], rd, os[r]);
+                if (rare & 1) {
 #pragma unroll
-                for (int g = 0; g < 2; ++g)
-                    if (id >= p.wd_lo[g] && id <= p.wd_hi[g]) {
-                        const auto rw = prs(p.D, id + p.wd_sh[g]);
+                    for (int g = 0; g < 2; ++g)
+                        if (id >= p.wd_lo[g] && id <= p.wd_hi[g]) {
+                            const auto rw = prs(p.D, id + p.wd_sh[g], pbytes);
 #pragma unroll
-                        for (int r = 0; r < R; ++r) bst<2>(d[S0][r], rw, os[r]);
-                    }
-                const bool erow = id >= p.ei0 && id <= p.ei1;
-                const T sx = ldconst(p.tx, id);
-#pragma unroll
-                for (int r = 0; r < R; ++r) {
-                    if (!ovalid[r]) continue;
-                    chk2 += d[S0][r];
-                    if (erow) accumulate_error_dev(d[S0][r], analytic(sx, oty[r], otz, p.ctD), ma2, mr2);
+                            for (int r = 0; r < R; ++r) bst<2>(d[S0][r], rw, os[r]);
+                        }
                 }
+                errors(d[S0], id, p.ctD, ma2, mr2, chk2);
             }
         }
 
@@ -352,24 +411,19 @@ __global__ void __launch_bounds__(NW * 64) k_tb3(const Tb3Params<T> p) {
                                           p.hx2, p.hy2, p.hz2, p.yx2, p.yy2, p.yz2);
                 ev[r] = leapfrog(d[S3][r], c[S2][r], lap, p.coefE);
             }
-            const auto re = prs(p.E, ie2);
+            const auto re = prs(p.E, ie2, pbytes);
 #pragma unroll
             for (int r = 0; r < R; ++r) bst<2>(ev[r], re, os[r]);
+            if (rare & 2) {
 #pragma unroll
-            for (int g = 0; g < 2; ++g)
-                if (ie2 >= p.we_lo[g] && ie2 <= p.we_hi[g]) {
-                    const auto rw = prs(p.E, ie2 + p.we_sh[g]);
+                for (int g = 0; g < 2; ++g)
+                    if (ie2 >= p.we_lo[g] && ie2 <= p.we_hi[g]) {
+                        const auto rw = prs(p.E, ie2 + p.we_sh[g], pbytes);
 #pragma unroll
-                    for (int r = 0; r < R; ++r) bst<2>(ev[r], rw, os[r]);
-                }
-            const bool erow = ie2 >= p.ei0 && ie2 <= p.ei1;
-            const T sx = ldconst(p.tx, ie2);
-#pragma unroll
-            for (int r = 0; r < R; ++r) {
-                if (!ovalid[r]) continue;
-                chk3 += ev[r];
-                if (erow) accumulate_error_dev(ev[r], analytic(sx, oty[r], otz, p.ctE), ma3, mr3);
+                        for (int r = 0; r < R; ++r) bst<2>(ev[r], rw, os[r]);
+                    }
             }
+            errors(ev, ie2, p.ctE, ma3, mr3, chk3);
         }
     };
 
@@ -437,6 +491,8 @@ static void (*tb3_kernel(int rows, int waves))(const Tb3Params<T>) {
         case 404: return k_tb3<T, F, 4, 4>;
         case 208: return k_tb3<T, F, 2, 8>;
         case 204: return k_tb3<T, F, 2, 4>;
+        case 116: return k_tb3<T, F, 1, 16>;
+        case 108: return k_tb3<T, F, 1, 8>;
         default: return nullptr;
     }
 }
@@ -448,15 +504,23 @@ bool tb3_supported(int rows, int waves) { return tb3_kernel<double, false>(rows,
 template <class T>
 void launch_tb3(int rows, int waves, bool first, const T* A, const T* B, T* D, T* E,
                 const GridView& gv, const Box* boxes, int nbox, const Box& cdom, int ei0, int ei1,
-                const Wrap& wrapD, const Wrap& wrapE, const SeamPartners<T>& seam, const T* tx,
-                const T* ty, const T* tz, const StepCoefs& cC, const StepCoefs& cD,
+                const Wrap& wrapD, const Wrap& wrapE, const SeamPartners<T>& seam, const T* txy,
+                const T* tz, const StepCoefs& cC, const StepCoefs& cD,
                 const StepCoefs& cE, u64* errC, u64* errD, u64* errE, int chunk, hipStream_t s) {
     W3D_REQUIRE(gv.G >= 3, "three-layer temporal blocking needs ghost depth >= 3");
     W3D_REQUIRE(tb3_supported(rows, waves), "tb3: unsupported rows x waves");
     W3D_REQUIRE(nbox >= 1 && nbox <= kMaxBoxes, "bad box count");
+    W3D_REQUIRE(gv.si * i64(sizeof(T)) < (i64(1) << 31), "tb3: plane larger than 2 GiB");
     Tb3Params<T> p{};
-    p.A = A, p.B = B, p.D = D, p.E = E;
-    p.si = gv.si;
+    // plane indices reach 1 - G (wrap targets) and ib - 3 >= -2
+    p.pbytes = unsigned(gv.si * i64(sizeof(T)));
+    p.pbias = gv.G + 1;
+    p.order = tile_order();
+    auto biased = [&](const T* base) {
+        return reinterpret_cast<char*>(reinterpret_cast<uintptr_t>(base - gv.poff) -
+                                       uintptr_t(p.pbias) * p.pbytes);
+    };
+    p.A = biased(A), p.B = biased(B), p.D = biased(D), p.E = biased(E);
     p.sj = gv.sj;
     p.poff = gv.poff;
     p.jmin = 1 - gv.G, p.jmax = gv.jmax(), p.kmin = 1 - gv.G, p.kmax = gv.kmax();
@@ -468,7 +532,7 @@ void launch_tb3(int rows, int waves, bool first, const T* A, const T* B, T* D, T
     p.ap_i = seam.pA ? seam.prev_i : INT_MIN / 2;
     W3D_REQUIRE((!seam.nA || seam.nC) && (!seam.pA || seam.pC), "tb3: seam partner without its C plane");
     p.nA = seam.nA, p.nC = seam.nC, p.pA = seam.pA, p.pC = seam.pC;
-    p.tx = tx, p.ty = ty, p.tz = tz;
+    p.txy = txy, p.tpj = gv.Y + 2, p.tz = tz;
     p.hx2 = T(cC.hx2), p.hy2 = T(cC.hy2), p.hz2 = T(cC.hz2);
     p.yx2 = T(1) / T(cC.hx2), p.yy2 = T(1) / T(cC.hy2), p.yz2 = T(1) / T(cC.hz2);
     p.coefC = T(cC.coef), p.coefD = T(cD.coef), p.coefE = T(cE.coef);
@@ -531,7 +595,7 @@ template void launch_seam_c<float>(bool, const SeamCPlane<float>*, int, const Gr
 #define W3D_TB3_INST(T)                                                                       \
     template void launch_tb3<T>(int, int, bool, const T*, const T*, T*, T*, const GridView&,  \
                                 const Box*, int, const Box&, int, int, const Wrap&,           \
-                                const Wrap&, const SeamPartners<T>&, const T*, const T*,      \
+                                const Wrap&, const SeamPartners<T>&, const T*,                \
                                 const T*, const StepCoefs&, const StepCoefs&,                 \
                                 const StepCoefs&, u64*, u64*, u64*, int, hipStream_t);
 W3D_TB3_INST(double)

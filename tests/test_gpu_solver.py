@@ -242,7 +242,7 @@ def test_temporal_blocking_3d_fp32_resume(C, tmp_path):
     assert res.max_abs == full.max_abs and res.max_rel == full.max_rel
 
 
-@pytest.mark.parametrize("kernel", ["tb3", "tb3r2w4", "tb3r4w4"])
+@pytest.mark.parametrize("kernel", ["tb3", "tb3r2w4", "tb3r4w4", "tb3r1w16", "tb3r1w8"])
 @pytest.mark.parametrize("K", [9, 10, 11])
 def test_tb3_single_rank_bitwise(C, kernel, K):
     """Three-layer temporal blocking (C never stored, seam partner planes from k_seam_c) with
@@ -265,9 +265,10 @@ def test_tb3_multi_rank_bitwise(C, ranks, dims, overlap):
     for K in (10, 12):
         p = wave3d.WaveProblem(47, Lx=1.3, Ly="pi", Lz=2.0, timesteps=K, ic="shifted")
         base = _solve(p, backend="cpu", threads=4)
-        r = _solve(p, ranks=ranks, dims=dims, overlap=overlap, kernel="tb3")
-        assert r.kernel == "tb3"
-        assert r.max_abs == base.max_abs and r.max_rel == base.max_rel
+        for kernel in ("tb3", "tb3r1w8"):
+            r = _solve(p, ranks=ranks, dims=dims, overlap=overlap, kernel=kernel)
+            assert r.kernel == kernel
+            assert r.max_abs == base.max_abs and r.max_rel == base.max_rel
 
 
 def test_tb3_fp32_resume_and_fault(C, tmp_path):

@@ -117,7 +117,7 @@ def test_tb2_sweep_matches_reference(C, dtype, first, rows, waves, kw, case):
 
 @pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
 @pytest.mark.parametrize("first", [False, True])
-@pytest.mark.parametrize("rows,waves", [(2, 8), (2, 4)])
+@pytest.mark.parametrize("rows,waves", [(2, 8), (2, 4), (1, 16), (1, 8)])
 @pytest.mark.parametrize("case", [0, 2, 3])
 def test_tb3_sweep_matches_reference(C, dtype, first, rows, waves, case):
     from wave3d.ops import kernels, reference
