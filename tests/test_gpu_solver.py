@@ -374,3 +374,18 @@ def test_tile_orders_bitwise(C, kernel):
         assert p.returncode == 0, p.stderr[-2000:]
         out[order] = json.loads(p.stdout.strip().splitlines()[-1])
     assert out["band"] == out["j"] == out["k"]
+
+
+def test_fp32_auto_is_tb3_bitwise(C):
+    """fp32 leapfrog "auto" runs three-layer blocking (tb3r2w8): bitwise equal to the OpenMP
+    fp32 oracle on one rank and on a 2x2x1 decomposition with overlap (3-deep halos)."""
+    import wave3d
+
+    p = wave3d.WaveProblem(40, timesteps=13, dtype="fp32", ic="shifted")
+    ref = _solve(p, "cpu")
+    got = _solve(p)
+    assert got.kernel == "tb3"
+    assert got.max_abs == ref.max_abs and got.max_rel == ref.max_rel
+    multi = _solve(p, ranks=4, dims=[2, 2, 1], overlap=True)
+    assert multi.kernel == "tb3"
+    assert multi.max_abs == ref.max_abs and multi.max_rel == ref.max_rel

@@ -27,9 +27,13 @@ def test_bytes_per_rank_matches_level_formula(C):
     level = (513 + 4) * (513 + 4) * sj * 8
     b = C.memory_plan(ARGS, 1)["bytes_per_rank"]
     assert 4 * level <= b < 4 * level * 1.01
-    # fp32 halves the levels; 8 slabs divide them by ~8
-    b32 = C.memory_plan(ARGS + ["--dtype", "fp32"], 1)["bytes_per_rank"]
-    assert 0.45 * b < b32 < 0.55 * b
+    # fp32 halves the level size; its auto kernel (tb3) keeps 5 levels with 3-deep ghosts
+    p32 = C.memory_plan(ARGS + ["--dtype", "fp32"], 1)
+    assert p32["tb"] and p32["ghost"] == 3 and p32["levels"] == 5
+    b32 = p32["bytes_per_rank"]
+    assert 0.60 * b < b32 < 0.70 * b
+    b32d = C.memory_plan(ARGS + ["--dtype", "fp32", "--scheme", "delta"], 1)["bytes_per_rank"]
+    assert 0.45 * b < b32d < 0.55 * b  # increment form: tb2, 4 levels
     assert C.memory_plan(ARGS, 8)["bytes_per_rank"] < b / 7
 
 
