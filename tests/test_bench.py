@@ -101,3 +101,15 @@ def test_bench_gpu_multirank_plan_staged(n, N, dims):
     assert r["config"]["transport"] == "staged.gloo" and r["rccl_nranks"] is None
     assert r["config"]["overlap"] is True and r["value"] > 0
     assert r["timers_ms"]["exchange_ms"] > 0
+
+
+@pytest.mark.gpu
+def test_bench_gpu_fp32_two_ranks_staged():
+    """fp32 runs the three-layer sweep (tb3, 3-deep halos) through the multi-process bench path:
+    2 processes on one MI355X, staged transport, N=512 on 2x1x1 slabs, K=100 (stable): the
+    fp32 L-inf of the single-GPU run (4.47035e-06, profiles/fp32_accuracy_r2.txt)."""
+    r = _bench(["--steps", "1", "--warmup", "0", "--dtype", "fp32", "--transport", "staged",
+                "--shared-device"], nproc=2, timeout=600)
+    assert r["dtype"] == "fp32" and r["n_gpus"] == 2 and r["config"]["dims"] == [2, 1, 1]
+    assert r["config"]["kernel"] == "tb3" and r["config"]["overlap"] is True
+    assert f"{r['linf_abs']:.6g}" == "4.47035e-06"
