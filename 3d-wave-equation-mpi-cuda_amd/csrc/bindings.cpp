@@ -238,7 +238,7 @@ void k_tb3_dense(int rows, int waves, bool first, uintptr_t A, uintptr_t B, uint
     if (hipMalloc(&txy, txy_elems(v.X, v.Y) * sizeof(T)) != hipSuccess) throw Error("k_tb3: hipMalloc failed");
     try {
         launch_txy<T>(txy, P<T>(tx), P<T>(ty), v.X, v.Y, s);
-        launch_tb3<T>(rows, waves, first, P<T>(A) + o, P<T>(B) + o, P<T>(D) + o, P<T>(E) + o, v,
+        launch_tb3<T>(rows, waves, false, first, P<T>(A) + o, P<T>(B) + o, P<T>(D) + o, P<T>(E) + o, v,
                       bx.data(), int(bx.size()), tobox(cdom), ei0, ei1, Wrap{}, Wrap{},
                       SeamPartners<T>{}, txy, P<T>(tz), tocoefs(cC), tocoefs(cD),
                       tocoefs(cE), P<u64>(errC), P<u64>(errD), P<u64>(errE), chunk, s);

@@ -140,7 +140,8 @@ public:
             // increment form: temporal blocking sweeps (u and d levels in the ring: after a
             // sweep, lvl(m+1) = u^{m+1}, lvl(m) = d^{m+1}); an odd last layer is one step of
             // the naive/flat kernel reading that d level
-            W3D_REQUIRE(tb_ && tbd_ == 2, "--scheme delta needs a tb2 kernel (kernel auto or tb2*)");
+            W3D_REQUIRE(tb_ && (tbd_ == 2 || tb3_delta_supported(tb_rows_, tb_waves_)),
+                        "--scheme delta needs a tb2 kernel or tb3 / tb3r1w8 (kernel auto, tb2*, tb3*)");
             kind_ = KernelVariant{};
             kind_.march = false;
             kind_.delta = true;
@@ -779,7 +780,7 @@ private:
     void seam_c(DevRank<T>& R, int m, hipStream_t s) {
         std::vector<SeamCPlane<T>> ops;
         seam_partners(R, m, &ops);
-        launch_seam_c<T>(m == 1, ops.data(), int(ops.size()), R.gv, R.cdom, coefs(m), s);
+        launch_seam_c<T>(m == 1, cfg_.delta, ops.data(), int(ops.size()), R.gv, R.cdom, coefs(m), s);
     }
 
     void sweep3(DevRank<T>& R, int m, hipStream_t s, const Box* boxes = nullptr, int nbox = 0) {
@@ -787,7 +788,7 @@ private:
         const T* B = R.g[lvl(m + L_ - 2)];
         const SeamPartners<T> sp = seam_partners(R, m, nullptr);
         if (!boxes) boxes = &R.compute, nbox = 1;
-        launch_tb3<T>(tb_rows_, tb_waves_, m == 1, A, B, R.g[lvl(m + 1)], R.g[lvl(m + 2)], R.gv, boxes,
+        launch_tb3<T>(tb_rows_, tb_waves_, cfg_.delta, m == 1, A, B, R.g[lvl(m + 1)], R.g[lvl(m + 2)], R.gv, boxes,
                       nbox, R.cdom, R.error.i0, R.error.i1, R.wrap2, R.wrap3, sp, R.txy, R.tz,
                       coefs(m), coefs(m + 1), coefs(m + 2), R.err + size_t(m) * kSlotsPerLayer,
                       R.err + size_t(m + 1) * kSlotsPerLayer, R.err + size_t(m + 2) * kSlotsPerLayer,

@@ -75,7 +75,11 @@ struct Tb3Params {
 // every thread owned one node of each ring (round 1), which put the fp64 kernel at 191-256 VGPRs.
 // WPE: minimum waves per SIMD the register allocation must allow (1-row tiles: 4, i.e. two
 // 8-wave or one 16-wave workgroup per CU).
-template <class T, bool FIRST, int R, int NW, int WPE = (R == 1 ? 4 : 1)>
+// DELTA: increment form (as k_tb2): B = d^{m-1}; d^m = B + coefC lap A, C = A + d^m;
+// d^{m+1} = d^m + coefD lap C, D = C + d^{m+1}; d^{m+2} = d^{m+1} + coefE lap D, E = D + d^{m+2}.
+// The D level receives d^{m+2} (the next sweep's B), so the bytes moved are unchanged.
+template <class T, bool FIRST, int R, int NW, bool DELTA = false,
+          int WPE = (R == 1 || (DELTA && sizeof(T) == 4) ? 4 : 1)>
 __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WPE, 8))) k_tb3(const Tb3Params<T> p) {
     constexpr int TJ = NW * R;
     constexpr int AH = TJ + 6, AW = kTK + 6;  // A tile origin (jt-3, kb-3)
@@ -193,6 +197,10 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WP
     //   B(x), ring B(x), LDS buffers: (x - ib + 2) & 1
     T a[4][R], c[4][R], d[4][R], bb[2][R];
     T ra[RP][4], rb[RP][2], rc[RP][4];
+    // increment form: d^m of own planes i (H0) / i-1 (H1) and of the ring, d^{m+1} of own
+    // planes i-1 (H0) / i-2 (H1)
+    constexpr int ND = DELTA ? 2 : 1;
+    T dm[ND][R], dm1[ND][R], rdm[RP][ND];
     {
         const auto r0 = prs(p.A, ib - 3, pbytes), rA1 = prs(p.A, ib - 2, pbytes), rA2 = prs(p.A, ib - 1, pbytes);
         const auto rB = prs(p.B, ib - 2, pbytes);
@@ -329,14 +337,27 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WP
         for (int r = 0; r < R; ++r) {
             const int y = 3 + w * R + r, x = 3 + lane;
             const T lap = lapA(H0, y, x, a[S1][r], xpA[r], xnA[r]);
-            c[S0][r] = ocd[r] ? cval(a[S1][r], bb[H0][r], lap) : T(0);
+            if constexpr (DELTA) {
+                const T dv = FIRST ? p.coefC * lap : delta_incr(bb[H0][r], lap, p.coefC);
+                dm[H0][r] = ocd[r] ? dv : T(0);
+                c[S0][r] = ocd[r] ? a[S1][r] + dv : T(0);  // FIRST: = taylor_first
+            } else {
+                c[S0][r] = ocd[r] ? cval(a[S1][r], bb[H0][r], lap) : T(0);
+            }
             ldsC[H0][y - 1][x - 1] = c[S0][r];
         }
 #pragma unroll
         for (int s = 0; s < RP; ++s) {
             if (rg[s] == 1 || rg[s] == 2) {
                 const T lap = lapA(H0, ry[s], rx[s], ra[s][S1], rxp[s], rxn[s]);
-                const T cv = rcd[s] ? cval(ra[s][S1], rb[s][H0], lap) : T(0);
+                T cv;
+                if constexpr (DELTA) {
+                    const T dv = FIRST ? p.coefC * lap : delta_incr(rb[s][H0], lap, p.coefC);
+                    rdm[s][H0] = rcd[s] ? dv : T(0);
+                    cv = rcd[s] ? ra[s][S1] + dv : T(0);
+                } else {
+                    cv = rcd[s] ? cval(ra[s][S1], rb[s][H0], lap) : T(0);
+                }
                 rc[s][S0] = cv;
                 ldsC[H0][ry[s] - 1][rx[s] - 1] = cv;
             }
@@ -369,7 +390,13 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WP
                 const T lap = laplace7_cr(c[S3][r], cpx[r], cnx[r], ldsC[H1][y - 1][x],
                                           ldsC[H1][y + 1][x], ldsC[H1][y][x - 1], ldsC[H1][y][x + 1],
                                           p.hx2, p.hy2, p.hz2, p.yx2, p.yy2, p.yz2);
-                d[S0][r] = ocd[r] ? leapfrog(c[S3][r], a[S0][r], lap, p.coefD) : T(0);
+                if constexpr (DELTA) {
+                    const T d1 = delta_incr(dm[H1][r], lap, p.coefD);  // d^{m+1}
+                    dm1[H0][r] = ocd[r] ? d1 : T(0);
+                    d[S0][r] = ocd[r] ? c[S3][r] + d1 : T(0);
+                } else {
+                    d[S0][r] = ocd[r] ? leapfrog(c[S3][r], a[S0][r], lap, p.coefD) : T(0);
+                }
                 ldsD[H0][y - 1][x - 1] = d[S0][r];
             }
 #pragma unroll
@@ -379,21 +406,26 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WP
                     const T lap = laplace7_cr(rc[s][S3], rcp[s], rcn[s], ldsC[H1][y - 1][x],
                                               ldsC[H1][y + 1][x], ldsC[H1][y][x - 1], ldsC[H1][y][x + 1],
                                               p.hx2, p.hy2, p.hz2, p.yx2, p.yy2, p.yz2);
-                    ldsD[H0][y - 1][x - 1] = rcd[s] ? leapfrog(rc[s][S3], ra[s][S0], lap, p.coefD) : T(0);
+                    if constexpr (DELTA)
+                        ldsD[H0][y - 1][x - 1] = rcd[s] ? rc[s][S3] + delta_incr(rdm[s][H1], lap, p.coefD) : T(0);
+                    else
+                        ldsD[H0][y - 1][x - 1] = rcd[s] ? leapfrog(rc[s][S3], ra[s][S0], lap, p.coefD) : T(0);
                 }
             }
             if (id >= ib && id <= ie) {
-                const auto rd = prs(p.D, id, pbytes);
+                if constexpr (!DELTA) {
+                    const auto rd = prs(p.D, id, pbytes);
 #pragma unroll
-                for (int r = 0; r < R; ++r) bst<2>(d[S0][r], rd, os[r]);
-                if (rare & 1) {
+                    for (int r = 0; r < R; ++r) bst<2>(d[S0][r], rd, os[r]);
+                    if (rare & 1) {
 #pragma unroll
-                    for (int g = 0; g < 2; ++g)
-                        if (id >= p.wd_lo[g] && id <= p.wd_hi[g]) {
-                            const auto rw = prs(p.D, id + p.wd_sh[g], pbytes);
+                        for (int g = 0; g < 2; ++g)
+                            if (id >= p.wd_lo[g] && id <= p.wd_hi[g]) {
+                                const auto rw = prs(p.D, id + p.wd_sh[g], pbytes);
 #pragma unroll
-                            for (int r = 0; r < R; ++r) bst<2>(d[S0][r], rw, os[r]);
-                        }
+                                for (int r = 0; r < R; ++r) bst<2>(d[S0][r], rw, os[r]);
+                            }
+                    }
                 }
                 errors(d[S0], id, p.ctD, ma2, mr2, chk2);
             }
@@ -409,7 +441,27 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WP
                 const T lap = laplace7_cr(d[S3][r], d[S2][r], d[S0][r], ldsD[H1][y - 1][x],
                                           ldsD[H1][y + 1][x], ldsD[H1][y][x - 1], ldsD[H1][y][x + 1],
                                           p.hx2, p.hy2, p.hz2, p.yx2, p.yy2, p.yz2);
-                ev[r] = leapfrog(d[S3][r], c[S2][r], lap, p.coefE);
+                if constexpr (DELTA) {
+                    dm1[H1][r] = delta_incr(dm1[H1][r], lap, p.coefE);  // d^{m+2}
+                    ev[r] = d[S3][r] + dm1[H1][r];
+                } else {
+                    ev[r] = leapfrog(d[S3][r], c[S2][r], lap, p.coefE);
+                }
+            }
+            if constexpr (DELTA) {
+                // d^{m+2} into the D level (+ its periodic self-wrap), the next sweep's B
+                const auto rd = prs(p.D, ie2, pbytes);
+#pragma unroll
+                for (int r = 0; r < R; ++r) bst<2>(dm1[H1][r], rd, os[r]);
+                if (rare & 2) {
+#pragma unroll
+                    for (int g = 0; g < 2; ++g)
+                        if (ie2 >= p.we_lo[g] && ie2 <= p.we_hi[g]) {
+                            const auto rw = prs(p.D, ie2 + p.we_sh[g], pbytes);
+#pragma unroll
+                            for (int r = 0; r < R; ++r) bst<2>(dm1[H1][r], rw, os[r]);
+                        }
+                }
             }
             const auto re = prs(p.E, ie2, pbytes);
 #pragma unroll
@@ -467,7 +519,7 @@ struct SeamCParams {
     T hx2, hy2, hz2, yx2, yy2, yz2, coef;
 };
 
-template <class T, bool FIRST>
+template <class T, bool FIRST, bool DELTA>
 __global__ void __launch_bounds__(kThreads) k_seam_c(const SeamCParams<T> p) {
     const SeamCOp<T> o = p.op[blockIdx.y];
     const int ktiles = (p.kmax - p.kmin - 1 + kTK - 1) / kTK;
@@ -480,7 +532,10 @@ __global__ void __launch_bounds__(kThreads) k_seam_c(const SeamCParams<T> p) {
         const T a = o.Ac[c];
         const T lap = laplace7_cr(a, o.Am[c], o.Ap[c], o.Ac[c - p.sj], o.Ac[c + p.sj], o.Ac[c - 1],
                                   o.Ac[c + 1], p.hx2, p.hy2, p.hz2, p.yx2, p.yy2, p.yz2);
-        v = FIRST ? taylor_first(a, lap, p.coef) : leapfrog(a, o.Bc[c], lap, p.coef);
+        if constexpr (DELTA)  // Bc = d^{m-1}
+            v = FIRST ? a + p.coef * lap : a + delta_incr(o.Bc[c], lap, p.coef);
+        else
+            v = FIRST ? taylor_first(a, lap, p.coef) : leapfrog(a, o.Bc[c], lap, p.coef);
     }
     o.out[c] = v;
 }
@@ -499,16 +554,29 @@ static void (*tb3_kernel(int rows, int waves))(const Tb3Params<T>) {
 
 }  // namespace
 
+// increment form: the 16-row and 1-row tiles (fp32 delta auto = r2w8: 537k vs tb2r2w8 520k Mpts/s
+// at N=512, profiles/tb3_diet_r2.txt)
+template <class T, bool F>
+static void (*tb3_delta_kernel(int rows, int waves))(const Tb3Params<T>) {
+    switch (rows * 100 + waves) {
+        case 208: return k_tb3<T, F, 2, 8, true>;
+        case 108: return k_tb3<T, F, 1, 8, true>;
+        default: return nullptr;
+    }
+}
+
 bool tb3_supported(int rows, int waves) { return tb3_kernel<double, false>(rows, waves) != nullptr; }
+bool tb3_delta_supported(int rows, int waves) { return tb3_delta_kernel<double, false>(rows, waves) != nullptr; }
 
 template <class T>
-void launch_tb3(int rows, int waves, bool first, const T* A, const T* B, T* D, T* E,
+void launch_tb3(int rows, int waves, bool delta, bool first, const T* A, const T* B, T* D, T* E,
                 const GridView& gv, const Box* boxes, int nbox, const Box& cdom, int ei0, int ei1,
                 const Wrap& wrapD, const Wrap& wrapE, const SeamPartners<T>& seam, const T* txy,
                 const T* tz, const StepCoefs& cC, const StepCoefs& cD,
                 const StepCoefs& cE, u64* errC, u64* errD, u64* errE, int chunk, hipStream_t s) {
     W3D_REQUIRE(gv.G >= 3, "three-layer temporal blocking needs ghost depth >= 3");
     W3D_REQUIRE(tb3_supported(rows, waves), "tb3: unsupported rows x waves");
+    W3D_REQUIRE(!delta || tb3_delta_supported(rows, waves), "tb3 increment form: tiles r2w8, r1w8 only");
     W3D_REQUIRE(nbox >= 1 && nbox <= kMaxBoxes, "bad box count");
     W3D_REQUIRE(gv.si * i64(sizeof(T)) < (i64(1) << 31), "tb3: plane larger than 2 GiB");
     Tb3Params<T> p{};
@@ -562,13 +630,14 @@ void launch_tb3(int rows, int waves, bool first, const T* A, const T* B, T* D, T
     }
     p.nbox = nb;
     if (nb == 0) return;
-    auto kern = first ? tb3_kernel<T, true>(rows, waves) : tb3_kernel<T, false>(rows, waves);
+    auto kern = delta ? (first ? tb3_delta_kernel<T, true>(rows, waves) : tb3_delta_kernel<T, false>(rows, waves))
+                      : (first ? tb3_kernel<T, true>(rows, waves) : tb3_kernel<T, false>(rows, waves));
     hipLaunchKernelGGL(kern, dim3(total), dim3(waves * 64), 0, s, p);
     HIP_OK(hipGetLastError());
 }
 
 template <class T>
-void launch_seam_c(bool first, const SeamCPlane<T>* ops, int nops, const GridView& gv,
+void launch_seam_c(bool first, bool delta, const SeamCPlane<T>* ops, int nops, const GridView& gv,
                    const Box& cdom, const StepCoefs& cC, hipStream_t s) {
     W3D_REQUIRE(nops >= 0 && nops <= 2, "seam C: at most two planes");
     if (nops == 0) return;
@@ -583,17 +652,18 @@ void launch_seam_c(bool first, const SeamCPlane<T>* ops, int nops, const GridVie
     p.coef = T(cC.coef);
     const int rows = p.jmax - p.jmin - 1, ktiles = cdiv(p.kmax - p.kmin - 1, kTK);
     const dim3 grid(cdiv(rows, kWaves) * ktiles, nops);
-    void (*kern)(const SeamCParams<T>) = first ? k_seam_c<T, true> : k_seam_c<T, false>;
+    void (*kern)(const SeamCParams<T>) = delta ? (first ? k_seam_c<T, true, true> : k_seam_c<T, false, true>)
+                                               : (first ? k_seam_c<T, true, false> : k_seam_c<T, false, false>);
     hipLaunchKernelGGL(kern, grid, dim3(kThreads), 0, s, p);
     HIP_OK(hipGetLastError());
 }
-template void launch_seam_c<double>(bool, const SeamCPlane<double>*, int, const GridView&, const Box&,
+template void launch_seam_c<double>(bool, bool, const SeamCPlane<double>*, int, const GridView&, const Box&,
                                     const StepCoefs&, hipStream_t);
-template void launch_seam_c<float>(bool, const SeamCPlane<float>*, int, const GridView&, const Box&,
+template void launch_seam_c<float>(bool, bool, const SeamCPlane<float>*, int, const GridView&, const Box&,
                                    const StepCoefs&, hipStream_t);
 
 #define W3D_TB3_INST(T)                                                                       \
-    template void launch_tb3<T>(int, int, bool, const T*, const T*, T*, T*, const GridView&,  \
+    template void launch_tb3<T>(int, int, bool, bool, const T*, const T*, T*, T*, const GridView&,  \
                                 const Box*, int, const Box&, int, int, const Wrap&,           \
                                 const Wrap&, const SeamPartners<T>&, const T*,                \
                                 const T*, const StepCoefs&, const StepCoefs&,                 \

@@ -33,10 +33,10 @@ Layout plan_layout(const Config& c, int world) {
     // grid is MPI_Dims_create's as in the reference (2x2x2 at 8 ranks; y/z splits get 2-deep
     // row/column halos); `--dims P,1,1` selects x slabs (contiguous planes, 2 peers)
     const bool auto_tb = c.kernel == "auto";
-    // fp32 leapfrog: three-layer blocking (tb3r2w8, 104 VGPRs / 4 waves per SIMD after the
-    // register diet) moves 10.7 instead of 16 B per node-layer and beats tb2r2w8 by 12-14 %
-    // (N=512 / 2048, profiles/tb3_diet_r2.txt); fp64 and the increment form stay on tb2
-    const bool auto_tb3 = auto_tb && c.dtype == DType::F32 && !c.delta;
+    // fp32: three-layer blocking (tb3r2w8, 4 waves per SIMD after the register diet) moves
+    // 10.7 instead of 16 B per node-layer and beats tb2r2w8 by 12-14 % (leapfrog) / 3-4 %
+    // (increment form), N=512 / 2048 (profiles/tb3_diet_r2.txt); fp64 stays on tb2
+    const bool auto_tb3 = auto_tb && c.dtype == DType::F32;
     const bool tb3 = auto_tb3 || c.kernel.rfind("tb3", 0) == 0;
     l.tb = auto_tb || tb3 || c.kernel.rfind("tb2", 0) == 0;
     l.depth = tb3 ? 3 : (l.tb ? 2 : 1);

@@ -306,14 +306,15 @@ def test_field_bitwise_vs_cpu(C, kernel, ranks, layer):
 @pytest.mark.parametrize("kernel,ranks,dims,overlap", [
     ("auto", 0, None, True), ("tb2", 0, None, True), ("tb2r4", 0, None, True),
     ("auto", 2, [2, 1, 1], True), ("tb2", 3, [3, 1, 1], False), ("auto", 8, [2, 2, 2], True),
-    ("tb2", 4, [1, 2, 2], False)])
+    ("tb2", 4, [1, 2, 2], False), ("tb3", 0, None, True), ("tb3r1w8", 0, None, True),
+    ("tb3", 2, [2, 1, 1], True), ("tb3", 8, [2, 2, 2], True), ("tb3r1w8", 4, [1, 2, 2], False)])
 def test_delta_scheme_matches_cpu(C, dtype, kernel, ranks, dims, overlap):
-    """Increment form on the HIP temporal-blocking path (u and d levels in the ring, an odd last
-    layer as one naive/flat step) == the OpenMP oracle's increment form, bit for bit, for even
-    and odd K, one rank, x slabs and 3-D blocks, with and without the overlap."""
+    """Increment form on the HIP temporal-blocking path (u and d levels in the ring; tb3: the D
+    level carries d^{m+2}; two-layer / single-step tails) == the OpenMP oracle's increment form,
+    bit for bit, for K = 10, 11, 12, one rank, x slabs and 3-D blocks, with and without overlap."""
     import wave3d
 
-    for K in (10, 11):
+    for K in (10, 11, 12):
         p = wave3d.WaveProblem(29, Lx=1.3, Ly="pi", Lz=2.0, timesteps=K, ic="shifted", dtype=dtype,
                                scheme="delta")
         ref = _solve(p, backend="cpu", threads=4)
