@@ -45,6 +45,9 @@ def main() -> int:
     ap.add_argument("--steps", type=int, default=5, help="timed solves")
     ap.add_argument("--warmup", type=int, default=2, help="untimed solves")
     ap.add_argument("--N", type=int, default=0, help="override global N (default: the BASELINE config)")
+    ap.add_argument("--config", default="",
+                    help="run a named BASELINE config instead (models/presets.py CONFIGS, e.g. "
+                         "gpu2048x8_fp32 = config 5: N, timesteps, dtype, decomposition)")
     ap.add_argument("--dims", default="", help="process grid a,b,c (default: the BASELINE config's)")
     ap.add_argument("--timesteps", type=int, default=100,
                     help="layers per solve (0: smallest stable count with margin, C <= 0.5)")
@@ -92,6 +95,19 @@ def main() -> int:
         torch.cuda.set_device(0)
 
     plan = presets.bench_plan(n_gpus)
+    if a.config:
+        if a.config not in presets.CONFIGS:
+            print(f"bench: unknown --config {a.config} ({', '.join(presets.CONFIGS)})", file=sys.stderr)
+            return 2
+        named = presets.CONFIGS[a.config]
+        if named["backend"] == "hip" and named["Np"] != n_gpus:
+            print(f"bench: --config {a.config} is a {named['Np']}-GPU config (running on {n_gpus})",
+                  file=sys.stderr)
+        np_ = named["problem"]
+        a.N, a.timesteps, a.dtype = np_.N, np_.timesteps, np_.dtype
+        if named["dims"] and not a.dims and named["Np"] == n_gpus:
+            a.dims = ",".join(str(x) for x in named["dims"])
+        plan = dict(plan, config=a.config, golden=presets.GOLDEN_LINF.get((np_.N, np_.timesteps)))
     N = a.N or plan["N"]
     dims = [int(x) for x in a.dims.split(",")] if a.dims else (None if a.N else plan["dims"])
     if a.fill_hbm > 0:
@@ -161,7 +177,7 @@ def main() -> int:
             "seq_len": N + 1,
             "parallelism": f"dd{dims[0]}x{dims[1]}x{dims[2]}-{res['kernel']}"
                            + ("" if n_gpus == 1 else f"-{res['transport']}"),
-            "baseline_config": None if a.N else plan["config"],
+            "baseline_config": a.config or (None if a.N else plan["config"]),
             "N": N,
             "timesteps": a.timesteps,
             "dims": dims,

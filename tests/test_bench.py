@@ -113,3 +113,12 @@ def test_bench_gpu_fp32_two_ranks_staged():
     assert r["dtype"] == "fp32" and r["n_gpus"] == 2 and r["config"]["dims"] == [2, 1, 1]
     assert r["config"]["kernel"] == "tb3" and r["config"]["overlap"] is True
     assert f"{r['linf_abs']:.6g}" == "4.47035e-06"
+
+
+def test_bench_named_config_cpu128():
+    """--config runs a BASELINE config by name (config 1: N=128 fp64 K=20 on the CPU backend)."""
+    r = _bench(["--backend", "cpu", "--config", "cpu128", "--steps", "1", "--warmup", "0"])
+    _check(r, 1, 1, 0)
+    assert r["config"]["N"] == 128 and r["config"]["timesteps"] == 20
+    assert r["config"]["baseline_config"] == "cpu128"
+    assert f"{r['linf_abs']:.6g}" == "8.81051e-06" and r["linf_ok"] is True
