@@ -94,6 +94,7 @@ py::dict result_dict(const Config& c, const RunResult& r) {
     d["graph"] = r.graph;
     d["overlap"] = r.overlap;
     d["comm_size"] = r.comm_size;
+    d["halo_checked"] = r.halo_checked;
     d["report"] = format_report(c, r);
     d["output_file"] = output_filename(c, r);
     d["json"] = json_summary(c, r);

@@ -33,7 +33,9 @@ std::string usage() {
            "  --graph on|off|auto    replay the time loop as one hipGraph (auto: when eligible)\n"
            "  --fill-hbm FRAC        GPU program: largest N whose per-GPU footprint fits FRAC of HBM\n"
            "  --dump PATH            write the final layer u^K as float64 .npy\n"
-           "  --fault SPEC           fault injection (drop_face:RANK:LAYER | nan:RANK:LAYER)\n"
+           "  --fault SPEC           fault injection (drop_face:RANK:LAYER | nan:RANK:LAYER |\n"
+           "                         corrupt_tag:RANK:TAG = halo self-test delivery of TAG to RANK)\n"
+           "  --no-halo-check        skip the init-time halo self-test (patterns through the real plan)\n"
            "  --device d  --threads t  --print-layers  --quiet\n";
 }
 
@@ -180,6 +182,8 @@ Config parse_cli(const std::vector<std::string>& a) {
             else if (v == "off") c.graph = 0;
             else if (v == "auto") c.graph = -1;
             else throw Error("--graph must be on, off or auto");
+        } else if (o == "--no-halo-check") {
+            c.halo_check = false;
         } else if (o == "--fault") {
             c.fault = need(i++);
         } else if (o == "--device") {

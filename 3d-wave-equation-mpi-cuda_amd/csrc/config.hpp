@@ -56,6 +56,7 @@ struct Config {
     bool profile = false;           // per-phase hipEvent timers
     int graph = -1;                 // hipGraph replay of the time loop: 1 on, 0 off, -1 auto
     double fill_hbm = 0;            // >0: replace N by the largest N using this HBM fraction
+    bool halo_check = true;         // init-time halo self-test through the real plan/transport
     std::string fault;              // fault injection spec, e.g. "drop_face:1:5" (or env WAVE_FI)
     int device = -1;                // explicit device id (default: local rank)
     int threads = 0;                // CPU backend OpenMP threads (0 = Np)

@@ -33,7 +33,7 @@ FaultSpec FaultSpec::parse(const std::string& s) {
     std::getline(ss, kind, ':');
     std::getline(ss, r, ':');
     std::getline(ss, n, ':');
-    W3D_REQUIRE(kind == "drop_face" || kind == "nan", "bad fault spec " + s);
+    W3D_REQUIRE(kind == "drop_face" || kind == "nan" || kind == "corrupt_tag", "bad fault spec " + s);
     f.kind = kind;
     f.rank = std::stoi(r);
     f.layer = std::stoi(n);

@@ -49,6 +49,20 @@ __device__ __forceinline__ T wave_max(T v) {
     return v;
 }
 
+__device__ __forceinline__ u64 wave_sum_u64(u64 v) {
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
+    return v;
+}
+__device__ __forceinline__ u64 wave_min_u64(u64 v) {
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+        const u64 o = __shfl_xor(v, off, 64);
+        v = o < v ? o : v;
+    }
+    return v;
+}
+
 // m = max(m, |d|) as one v_max with an abs source modifier. fmax() of a loop-carried value
 // costs two extra canonicalising v_max per node (plus a v_and for the |.|); the raw
 // instruction in IEEE mode already returns the other operand for a quiet-NaN input, and every

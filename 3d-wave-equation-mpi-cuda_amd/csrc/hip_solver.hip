@@ -21,6 +21,7 @@
 
 #include "checkpoint.hpp"
 #include "hip_kernels.hpp"
+#include "hip_selftest.hpp"
 #include "problem.hpp"
 #include "sizing.hpp"
 #include "solver.hpp"
@@ -161,8 +162,10 @@ public:
         TraceRange tr("wave3d.setup");
         auto t0 = clk::now();
         setup();
-        bool halos = fault_.kind == "drop_face";
-        for (auto& R : ranks_) halos |= !R.plan.sends.empty() || tb_halo(R);
+        bool msgs = false;
+        for (auto& R : ranks_) msgs |= !R.plan.sends.empty() || !R.plan.recvs.empty() || tb_halo(R);
+        if (msgs && cfg_.halo_check) halo_self_test();
+        const bool halos = msgs || fault_.kind == "drop_face";
         fine_ = cfg_.profile || halos;
         // every mark of a solve: IC + per sweep (compute, exchange) + reduction
         ts_cap_ = size_t(6) * (prob_.K + 4) + 16;
@@ -210,6 +213,7 @@ public:
         res.overlap = overlap_;
         res.scheme = cfg_.delta ? "delta" : "leapfrog";
         res.comm_size = ext_ ? ext_->comm_size() : 0;
+        res.halo_checked = halo_checked_;
         for (int a = 0; a < 3; ++a) res.dims[a] = ranks_[0].topo.dims[a];
         Timings t;
         solve(res, t);
@@ -812,6 +816,7 @@ private:
     }
 
     void inject_after_exchange(DevRank<T>& R, int n, hipStream_t s) {
+        if (selftest_) return;
         // exchanges follow every sweep: a fault layer inside the sweep hits its exchange
         const int lo = tbd_ == 3 ? n - 3 : (tb_ ? n - 2 : n - 1);
         if (fault_.kind == "drop_face" && fault_.hits_range(R.topo.rank, lo, n))
@@ -864,6 +869,176 @@ private:
             pack_faces(R, n, s, false);
             inject_after_exchange(R, n, s);
         }
+    }
+
+    // ---- init-time halo self-test ---------------------------------------------------------
+    // One real exchange of position-encoded patterns (hip_selftest.hpp) through this run's
+    // plan and transport — x planes, seam alias planes, y/z box rounds, or the single-step
+    // faces — and a device check of every cell each message delivered. A wrong peer, tag,
+    // size, level or placement fails at setup with the rank, peer and tag of the message; the
+    // failure count is max-reduced over the ranks so every rank stops at once (the reference
+    // only ever sees a halo bug as a wrong error table, cuda_sol.cpp:245-310).
+    struct CheckRegion {
+        int peer = -1, tag = 0;
+        const T* origin = nullptr;  // logical (0,0,0) of the level / alias plane
+        Box box;
+        PatternCoords pc;
+        std::string what;
+    };
+
+    std::vector<CheckRegion> check_regions(DevRank<T>& R, bool deep, int lA, int lB, unsigned sA, unsigned sB) {
+        std::vector<CheckRegion> out;
+        const auto& t = R.topo;
+        const int X = t.X(), Y = t.Y(), Z = t.Z();
+        PatternCoords base;
+        for (int a = 0; a < 3; ++a) base.off[a] = t.off[a];
+        base.N = prob_.N;
+        auto region = [&](int peer, int tag, const T* origin, Box b, unsigned salt, i64 gi, std::string what) {
+            CheckRegion c;
+            c.peer = peer, c.tag = tag, c.origin = origin, c.box = b, c.pc = base;
+            c.pc.salt = salt, c.pc.gi_fixed = gi, c.what = std::move(what);
+            out.push_back(c);
+        };
+        if (!deep) {
+            const int l = lvl(1);
+            for (const auto& f : R.plan.recvs) {
+                Box b{1, X, 1, Y, 1, Z};
+                const int ghost = f.side ? t.ext[f.axis] + 1 : 0;
+                if (f.axis == 0) b.i0 = b.i1 = ghost;
+                else if (f.axis == 1) b.j0 = b.j1 = ghost;
+                else b.k0 = b.k1 = ghost;
+                region(f.peer, f.tag, R.g[l], b, sA, -1, std::string("face axis ") + "xyz"[f.axis]);
+            }
+            return out;
+        }
+        const i64 alias_gi = t.first(0) ? prob_.N : 0;  // first x-rank holds x=N, last x=0
+        for (const auto& m : R.tb_recvs) {
+            const unsigned salt = m.level == 0 ? sA : sB;
+            if (m.plane == kAliasPlane) {
+                const T* o = (m.level == 0 ? R.alias_buf : R.alias_bufB) + R.plane_off;
+                region(m.peer, m.tag, o, Box{0, 0, 1, Y, 1, Z}, salt, alias_gi, "seam alias plane");
+            } else {
+                region(m.peer, m.tag, R.g[m.level == 0 ? lA : lB],
+                       Box{m.plane, m.plane + m.nplanes - 1, 1, Y, 1, Z}, salt, -1, "x planes");
+            }
+        }
+        const int dA = tbd_, dB = tbd_ - 1;
+        for (int rd = 0; rd < 2; ++rd)
+            for (const auto& m : R.tb_brecvs[rd]) {
+                // only what the sender itself held valid: ghosts of depth dA (A) / dB (B) on
+                // the axes exchanged before; a fused local x wrap is not part of the exchange
+                const int d = m.level == 1 ? dB : dA;
+                Box b = m.box;
+                if (m.level != 2) {
+                    b.i0 = std::max(b.i0, R.plan.self_x ? 1 : 1 - d);
+                    b.i1 = std::min(b.i1, R.plan.self_x ? X : X + d);
+                }
+                b.j0 = std::max(b.j0, 1 - d), b.j1 = std::min(b.j1, Y + d);
+                b.k0 = std::max(b.k0, 1 - d), b.k1 = std::min(b.k1, Z + d);
+                if (m.level == 2)
+                    region(m.peer, m.tag, R.alias_buf + R.plane_off, b, sA, alias_gi, "alias plane box");
+                else
+                    region(m.peer, m.tag, R.g[m.level == 0 ? lA : lB], b, m.level == 0 ? sA : sB, -1,
+                           rd == 0 ? "y box" : "z box");
+            }
+        return out;
+    }
+
+    void halo_self_test() {
+        TraceRange tr("wave3d.halo_selftest");
+        const bool deep = tb_ && tb_halo(ranks_[0]);
+        const int mD = 2;  // deep: A level = lvl(2), B = lvl(1) (as exchange_tb); faces: lvl(1)
+        const int lA = deep ? lvl(mD) : lvl(1), lB = lvl(mD - 1 + L_);
+        const unsigned sA = 0xA11CEu, sB = 0xB0B5u;
+        hipStream_t s = s_comp_;
+        std::vector<std::vector<CheckRegion>> regs;
+        size_t nreg = 0;
+        for (auto& R : ranks_) {
+            PatternCoords pc;
+            for (int a = 0; a < 3; ++a) pc.off[a] = R.topo.off[a];
+            pc.N = prob_.N;
+            const Box all{1 - G_, R.topo.X() + G_, 1 - G_, R.topo.Y() + G_, 1 - G_, R.topo.Z() + G_};
+            pc.salt = sA;
+            launch_pattern_fill<T>(R.g[lA], R.gv, all, pc, 0, 0.0, s);
+            if (deep) {
+                pc.salt = sB;
+                launch_pattern_fill<T>(R.g[lB], R.gv, all, pc, 0, 0.0, s);
+                if (R.alias_buf) HIP_CHECK(hipMemsetAsync(R.alias_buf, 0, R.gv.si * sizeof(T), s));
+                if (R.alias_bufB) HIP_CHECK(hipMemsetAsync(R.alias_bufB, 0, R.gv.si * sizeof(T), s));
+            } else {
+                pack_faces(R, 1, s, true);
+            }
+            regs.push_back(check_regions(R, deep, lA, lB, sA, sB));
+            nreg += regs.back().size();
+        }
+        selftest_ = true;  // no --fault drop_face injection into the test exchange
+        if (deep) exchange_tb(mD, s);
+        else exchange(1, s);
+        selftest_ = false;
+        // fault hook (--fault corrupt_tag:RANK:TAG): what the message of that tag delivered to
+        // RANK is overwritten, as a transport that lost or misrouted it would leave it
+        for (size_t q = 0; q < ranks_.size(); ++q)
+            if (fault_.kind == "corrupt_tag" && ranks_[q].topo.rank == fault_.rank)
+                for (auto& c : regs[q])
+                    if (c.tag == fault_.layer)
+                        launch_pattern_fill<T>(const_cast<T*>(c.origin), ranks_[q].gv, c.box, c.pc, 1, 0.0, s);
+        u64* dres = nullptr;
+        HIP_CHECK(hipMalloc(&dres, sizeof(u64) * 2 * std::max<size_t>(1, nreg)));
+        std::vector<u64> init(2 * std::max<size_t>(1, nreg));
+        for (size_t q = 0; q < init.size(); ++q) init[q] = q % 2 ? ~0ull : 0ull;
+        HIP_CHECK(hipMemcpyAsync(dres, init.data(), init.size() * sizeof(u64), hipMemcpyHostToDevice, s));
+        size_t idx = 0;
+        for (size_t q = 0; q < ranks_.size(); ++q)
+            for (auto& c : regs[q]) launch_pattern_check<T>(c.origin, ranks_[q].gv, c.box, c.pc, dres + 2 * idx++, s);
+        std::vector<u64> res(init.size());
+        HIP_CHECK(hipMemcpyAsync(res.data(), dres, res.size() * sizeof(u64), hipMemcpyDeviceToHost, s));
+        sync(s);
+        std::string report;
+        int nbad = 0;
+        idx = 0;
+        for (size_t q = 0; q < ranks_.size(); ++q)
+            for (auto& c : regs[q]) {
+                const u64 bad = res[2 * idx], first = res[2 * idx + 1];
+                ++idx;
+                if (!bad) continue;
+                ++nbad;
+                const Box& b = c.box;
+                const i64 nk = b.k1 - b.k0 + 1, nj = b.j1 - b.j0 + 1;
+                const int k = b.k0 + int(i64(first) % nk), j = b.j0 + int(i64(first) / nk % nj),
+                          i = b.i0 + int(i64(first) / nk / nj);
+                T got{};
+                HIP_CHECK(hipMemcpy(&got, c.origin + i64(i) * ranks_[q].gv.si + i64(j) * ranks_[q].gv.sj + k,
+                                    sizeof(T), hipMemcpyDeviceToHost));
+                i64 gi = c.pc.gi_fixed >= 0 ? c.pc.gi_fixed : c.pc.off[0] + i - 1;
+                const i64 gj = c.pc.off[1] + j - 1, gk = c.pc.off[2] + k - 1, N = prob_.N;
+                gi = gi < 0 ? gi + N : (gi > N ? gi - N : gi);
+                const double want = (gj < 0 || gj > N || gk < 0 || gk > N)
+                                        ? kPatternSentinel
+                                        : double(T(halo_pattern_value(gi, gj, gk, c.pc.salt)));
+                if (nbad <= 8)
+                    report += "\n  rank " + std::to_string(ranks_[q].topo.rank) + ": message from peer " +
+                              std::to_string(c.peer) + " tag " + std::to_string(c.tag) + " (" + c.what + "): " +
+                              std::to_string(bad) + " of " + std::to_string(b.count()) +
+                              " cells wrong, first at local (" + std::to_string(i) + "," + std::to_string(j) +
+                              "," + std::to_string(k) + "): got " + std::to_string(double(got)) + " expected " +
+                              std::to_string(want);
+            }
+        (void)hipFree(dres);
+        double v = nbad;
+        if (ext_) ext_->allreduce_max_host(&v, 1);  // every rank fails together, fast
+        // restore the post-allocation state the solve relies on (zeroed levels and alias planes)
+        for (auto& R : ranks_) {
+            for (int l = 0; l < L_; ++l) HIP_CHECK(hipMemsetAsync(R.alloc[l], 0, R.elems * sizeof(T), s));
+            if (R.alias_buf) HIP_CHECK(hipMemsetAsync(R.alias_buf, 0, R.gv.si * sizeof(T), s));
+            if (R.alias_bufB) HIP_CHECK(hipMemsetAsync(R.alias_bufB, 0, R.gv.si * sizeof(T), s));
+        }
+        sync(s);
+        if (v > 0)
+            throw Error("wave3d: halo self-test failed" +
+                        (report.empty() ? std::string(" on another rank (this rank's messages were correct)")
+                                        : ":" + report));
+        halo_checked_ = int(nreg);
+        log_msg(LogLevel::Info, "halo self-test: ", nreg, " messages verified");
     }
 
     // Phase timers (the reference's C26 breakdown, mpi_new.cpp:33-34,368-371, in every run):
@@ -1359,6 +1534,8 @@ private:
     int L_ = 3;         // time levels kept
     bool overlap_ = false;
     bool xself_ = false;  // --x-self-transport
+    bool selftest_ = false;  // inside halo_self_test()
+    int halo_checked_ = 0;   // messages verified by the init-time halo self-test
     int world_ = 1;
     std::vector<int> local_;
     std::vector<DevRank<T>> ranks_;

@@ -94,7 +94,7 @@ std::string json_summary(const Config& c, const RunResult& r) {
       << "\", \"kernel\": \"" << r.kernel << "\", \"scheme\": \"" << r.scheme
       << "\", \"transport\": \"" << r.transport << "\""
       << ", \"overlap\": " << (r.overlap ? "true" : "false")
-      << ", \"comm_size\": " << r.comm_size
+      << ", \"comm_size\": " << r.comm_size << ", \"halo_checked\": " << r.halo_checked
       << ", \"courant\": " << jnum(r.courant) << ", \"total_ms\": " << jnum(r.t.total_ms)
       << ", \"init_ms\": " << jnum(r.t.init_ms) << ", \"loop_ms\": " << jnum(r.t.loop_ms)
       << ", \"exchange_ms\": " << jnum(r.t.exchange_ms) << ", \"comm_ms\": " << jnum(r.t.comm_ms)

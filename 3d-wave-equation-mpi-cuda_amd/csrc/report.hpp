@@ -39,6 +39,7 @@ struct RunResult {
     bool graph = false;  // time loop replayed as one hipGraph
     bool overlap = false;  // interior/shell split with the halo on a second stream (effective)
     int comm_size = 0;     // ranks the transport's communicator reports (ncclCommCount), 0 = none
+    int halo_checked = 0;  // halo messages verified by the init-time self-test (0 = none ran)
 
     double points() const { return double(N + 1) * double(N + 1) * double(N + 1); }
     // Mpoints/s = (N+1)^3 * timesteps / t  (BASELINE.md metric definition)

@@ -53,7 +53,7 @@ RunResult run_hip(const Config& c, Transport* external = nullptr);
 
 // Fault-injection spec parsed from --fault / WAVE_FI.
 struct FaultSpec {
-    std::string kind;  // "" | "drop_face" | "nan"
+    std::string kind;  // "" | "drop_face" | "nan" | "corrupt_tag" (layer = the halo tag)
     int rank = -1;
     int layer = -1;
     static FaultSpec parse(const std::string& s);

@@ -62,7 +62,14 @@ def main() -> int:
     ap.add_argument("--transport", default="rccl", choices=["rccl", "staged"],
                     help="halo transport for N>1 (staged = rehearsal on one shared GPU)")
     ap.add_argument("--shared-device", action="store_true", help="all ranks on device 0 (rehearsal)")
+    ap.add_argument("--launch-timeout", type=float, default=1000.0,
+                    help="self-launch (--gpus N without torchrun): kill every rank after this many s")
     a = ap.parse_args()
+
+    if "WORLD_SIZE" not in os.environ and a.gpus > 1:
+        # one command, N ranks (the reference's `mpirun -n Np`, README.txt:43): spawn the ranks
+        # as child processes before this process touches torch or the GPU
+        return launch_ranks(a.gpus, sys.argv[1:], a.launch_timeout)
 
     import torch
     import torch.distributed as dist
@@ -76,17 +83,27 @@ def main() -> int:
     if world != a.gpus and world > 1:
         print(f"bench: WORLD_SIZE={world} but --gpus {a.gpus}", file=sys.stderr)
     n_gpus = world if world > 1 else a.gpus
-    if world == 1 and a.gpus > 1:
-        print("bench: --gpus > 1 must be launched with torch.distributed.run (one rank per GPU)",
-              file=sys.stderr)
-        return 2
 
     transport = None
     if world > 1:
         if a.backend == "hip":
-            torch.cuda.set_device(0 if a.shared_device else local % torch.cuda.device_count())
+            # preflight before any communicator exists: one GPU per rank (RCCL refuses two
+            # ranks on one device; --shared-device rehearses on one GPU with --transport staged)
+            ndev = torch.cuda.device_count()
+            if ndev == 0 or (not a.shared_device and ndev < world):
+                print(f"bench: rank {rank}: {world} ranks need {world} GPUs, {ndev} visible "
+                      "(--shared-device --transport staged rehearses on one GPU)", file=sys.stderr)
+                return 2
+            if a.shared_device and a.transport == "rccl":
+                print("bench: --shared-device needs --transport staged (RCCL refuses duplicate GPUs)",
+                      file=sys.stderr)
+                return 2
+            torch.cuda.set_device(0 if a.shared_device else local % ndev)
         nccl = a.backend == "hip" and a.transport == "rccl"
         wdist.init_from_env("nccl" if nccl else "gloo")
+        if os.environ.get("WAVE3D_BENCH_FAIL_RANK") == str(rank):  # test hook: a rank dies
+            print(f"bench: rank {rank}: WAVE3D_BENCH_FAIL_RANK", file=sys.stderr)
+            return 3
         if a.backend == "hip":
             transport = wdist.make_transport(a.transport)
         else:
@@ -191,6 +208,9 @@ def main() -> int:
         },
         # ranks the halo communicator spans as RCCL reports them (ncclCommCount), None without one
         "rccl_nranks": res["comm_size"] if res["transport"] == "rccl" else None,
+        # halo messages checked at setup with position-encoded patterns (hip_solver.hip)
+        "halo_checked": res.get("halo_checked", 0),
+        "launch": "self" if os.environ.get("WAVE3D_SELF_LAUNCH") else ("torchrun" if world > 1 else "single"),
         "linf_abs": res["linf_abs"],
         "linf_final_layer": res["timesteps"],
         "linf_golden": golden,
@@ -213,6 +233,84 @@ def main() -> int:
         dist.barrier()
         dist.destroy_process_group()
     return 0
+
+
+def _free_port() -> int:
+    import socket
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def launch_ranks(n: int, argv: list[str], timeout: float) -> int:
+    """Run this script as `n` ranks (children with torchrun's env: RANK, WORLD_SIZE,
+    LOCAL_RANK, LOCAL_WORLD_SIZE, MASTER_ADDR=127.0.0.1, MASTER_PORT) and relay rank 0's stdout.
+    The parent never imports torch or touches a GPU. The first rank to fail (or the timeout)
+    ends the job: the other ranks are terminated at once instead of waiting in a collective,
+    and the exit status is the failed rank's."""
+    import signal
+    import subprocess
+    import threading
+
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(n), LOCAL_RANK=str(r),
+                   LOCAL_WORLD_SIZE=str(n), GROUP_RANK="0", MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port), WAVE3D_SELF_LAUNCH="1")
+        procs.append(subprocess.Popen([sys.executable, "-u", os.path.abspath(__file__)] + argv, env=env,
+                                      stdout=subprocess.PIPE if r == 0 else subprocess.DEVNULL,
+                                      start_new_session=True, text=True))
+
+    def relay():
+        for line in procs[0].stdout:
+            sys.stdout.write(line)
+            sys.stdout.flush()
+
+    th = threading.Thread(target=relay, daemon=True)
+    th.start()
+
+    def stop_all():
+        for p in procs:
+            if p.poll() is None:
+                try:
+                    os.killpg(p.pid, signal.SIGTERM)
+                except ProcessLookupError:
+                    pass
+        t_end = time.time() + 10
+        for p in procs:
+            try:
+                p.wait(timeout=max(0.1, t_end - time.time()))
+            except subprocess.TimeoutExpired:
+                try:
+                    os.killpg(p.pid, signal.SIGKILL)
+                except ProcessLookupError:
+                    pass
+                p.wait()
+
+    t0 = time.time()
+    rc = 0
+    while True:
+        codes = [p.poll() for p in procs]
+        failed = [(r, c) for r, c in enumerate(codes) if c not in (None, 0)]
+        if failed:
+            r, rc = failed[0]
+            print(f"bench: rank {r} exited with status {rc}; stopping the other ranks", file=sys.stderr)
+            stop_all()
+            break
+        if all(c == 0 for c in codes):
+            break
+        if time.time() - t0 > timeout:
+            print(f"bench: ranks still running after {timeout:.0f} s; stopping them", file=sys.stderr)
+            stop_all()
+            rc = 124
+            break
+        time.sleep(0.05)
+    th.join(timeout=5)
+    return rc if rc > 0 else (1 if rc < 0 else 0)
 
 
 if __name__ == "__main__":

@@ -21,8 +21,10 @@ def _port():
     return p
 
 
-def _bench(extra, nproc=1, timeout=300):
-    if nproc == 1:
+def _bench(extra, nproc=1, timeout=300, self_launch=False):
+    if self_launch:
+        cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(nproc)] + extra
+    elif nproc == 1:
         cmd = [sys.executable, os.path.join(ROOT, "bench.py")] + extra
     else:
         cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
@@ -122,3 +124,41 @@ def test_bench_named_config_cpu128():
     assert r["config"]["N"] == 128 and r["config"]["timesteps"] == 20
     assert r["config"]["baseline_config"] == "cpu128"
     assert f"{r['linf_abs']:.6g}" == "8.81051e-06" and r["linf_ok"] is True
+
+
+def test_bench_self_launch_cpu_two_ranks():
+    """`python bench.py --gpus 2` without torchrun spawns its own two ranks (the reference's
+    one-command `mpirun -n Np`, README.txt:43) and relays rank 0's JSON line."""
+    r = _bench(["--backend", "cpu", "--N", "32", "--timesteps", "20", "--steps", "1", "--warmup", "0"],
+               nproc=2, self_launch=True)
+    _check(r, 2, 1, 0)
+    assert r["launch"] == "self" and r["config"]["dims"] == [2, 1, 1]
+    assert f"{r['linf_abs']:.6g}" == "0.000175963" and r["linf_ok"] is True
+
+
+def test_bench_self_launch_fails_fast():
+    """One rank dying makes the self-launched job exit with that rank's status at once (the
+    other ranks sit in a collective and are terminated instead of waiting for a timeout)."""
+    import time
+
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "3", "--backend", "cpu", "--N", "32",
+           "--timesteps", "20", "--steps", "1", "--warmup", "0"]
+    t0 = time.time()
+    out = subprocess.run(cmd, capture_output=True, text=True, cwd=ROOT, timeout=120,
+                         env=dict(os.environ, WAVE3D_BENCH_FAIL_RANK="1"))
+    assert out.returncode == 3, out.stderr[-2000:]
+    assert "rank 1 exited with status 3" in out.stderr
+    assert time.time() - t0 < 60
+
+
+@pytest.mark.gpu
+def test_bench_gpu_self_launch_two_ranks_staged():
+    """The multi-GPU bench as one command: 2 self-launched ranks on one MI355X (staged
+    transport), the BASELINE 2-GPU config (N=512, 2x1x1, K=100) at the golden L-inf, with the
+    init-time halo self-test through the real plan."""
+    r = _bench(["--steps", "1", "--warmup", "0", "--transport", "staged", "--shared-device"], nproc=2,
+               timeout=600, self_launch=True)
+    _check(r, 2, 1, 0)
+    assert r["launch"] == "self" and r["config"]["N"] == 512 and r["config"]["dims"] == [2, 1, 1]
+    assert r["config"]["timesteps"] == 100 and r["linf_ok"] is True
+    assert r["halo_checked"] > 0

@@ -1,0 +1,64 @@
+"""Init-time halo self-test (hip_solver.hip halo_self_test, hip_selftest.hip).
+
+Every run that moves halos first sends position-encoded patterns through its real plan and
+transport and checks every delivered cell on the device. These tests run it on the plans of
+every decomposition shape and kernel family (single-step faces, two- and three-layer deep
+halos with seam alias planes and y/z box rounds) and check that a corrupted delivery fails the
+run at setup, naming the rank, peer and tag, within seconds."""
+import json
+import subprocess
+import time
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ARGS = ["40", "1", "pi", "pi", "pi", "1", "12"]
+
+CASES = [
+    # (dims, kernel, dtype, a tag the plan delivers to rank 1)
+    ("2,1,1", "march2", "fp64", 1),
+    ("2,2,2", "march2", "fp64", 4),
+    ("1,2,2", "march2", "fp64", 5),
+    ("2,1,1", "tb2", "fp64", 11),
+    ("2,2,2", "tb2", "fp64", 61),
+    ("1,2,2", "tb2", "fp64", 32),
+    ("4,1,1", "tb3", "fp64", 13),
+    ("2,2,2", "tb3", "fp32", 63),
+    ("1,2,2", "tb3", "fp32", 31),
+]
+
+
+def _run(gpu_prog, dims, kernel, dtype, extra=()):
+    P = 1
+    for d in dims.split(","):
+        P *= int(d)
+    cmd = [gpu_prog] + ARGS + ["--ranks", str(P), "--dims", dims, "--kernel", kernel, "--dtype", dtype,
+                               "--json", "--quiet", "--format", "none"] + list(extra)
+    t0 = time.time()
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=120)
+    return out, time.time() - t0
+
+
+@pytest.mark.parametrize("dims,kernel,dtype,tag", CASES)
+def test_halo_selftest_passes(gpu_prog, dims, kernel, dtype, tag):
+    out, _ = _run(gpu_prog, dims, kernel, dtype)
+    assert out.returncode == 0, out.stderr[-2000:]
+    r = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][0])
+    assert r["halo_checked"] > 0 and r["kernel"].startswith(kernel[:3])
+
+
+@pytest.mark.parametrize("dims,kernel,dtype,tag", CASES)
+def test_halo_selftest_names_corrupted_tag(gpu_prog, dims, kernel, dtype, tag):
+    out, dt = _run(gpu_prog, dims, kernel, dtype, ["--fault", f"corrupt_tag:1:{tag}"])
+    assert out.returncode != 0
+    assert "halo self-test failed" in out.stderr, out.stderr[-2000:]
+    assert f"rank 1: message from peer" in out.stderr and f" tag {tag} " in out.stderr, out.stderr[-2000:]
+    assert dt < 60
+
+
+def test_halo_selftest_can_be_skipped(gpu_prog):
+    out, _ = _run(gpu_prog, "2,1,1", "tb2", "fp64", ["--no-halo-check", "--fault", "corrupt_tag:1:11"])
+    assert out.returncode == 0, out.stderr[-2000:]
+    r = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][0])
+    assert r["halo_checked"] == 0
