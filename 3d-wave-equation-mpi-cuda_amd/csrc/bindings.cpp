@@ -10,6 +10,7 @@
 #include <pybind11/pybind11.h>
 
 #include <chrono>
+#include <thread>
 #include <pybind11/stl.h>
 
 #include "checkpoint.hpp"
@@ -425,6 +426,36 @@ PYBIND11_MODULE(_wave3d_C, m) {
                     limit_s, [&] { aborted = true; }, "probe");
         return el();
     }, py::arg("limit_s"), py::arg("done_after_s"), py::arg("progress_until_s"));
+    // thread-per-GPU failure handling without a GPU: rank `fail_rank` throws after
+    // `fail_after_s`, every other rank waits in watch_until (as on an RCCL stream) with a
+    // `limit_s` watchdog; returns (seconds, error) per rank
+    m.def("abort_probe", [](int n, int fail_rank, double fail_after_s, double limit_s) {
+        using clk = std::chrono::steady_clock;
+        const auto t0 = clk::now();
+        auto el = [&] { return std::chrono::duration<double>(clk::now() - t0).count(); };
+        std::vector<double> t(n, 0.0);
+        std::vector<std::string> errs;
+        {
+            py::gil_scoped_release nogil;
+            errs = run_rank_threads(n, [&](int r) {
+                if (r == fail_rank) {
+                    std::this_thread::sleep_for(std::chrono::duration<double>(fail_after_s));
+                    t[r] = el();
+                    throw Error("injected failure");
+                }
+                try {
+                    watch_until([] { return false; }, [] { return std::string(); }, nullptr, limit_s, [] {},
+                                "probe");
+                } catch (...) {
+                    t[r] = el();
+                    throw;
+                }
+            });
+        }
+        py::list out;
+        for (int r = 0; r < n; ++r) out.append(py::make_tuple(t[r], errs[r]));
+        return out;
+    }, py::arg("n"), py::arg("fail_rank"), py::arg("fail_after_s"), py::arg("limit_s"));
     m.def("checkpoint_layers", &checkpoint_layers, py::arg("dir"), py::arg("rank"),
           "Layers with a complete checkpoint file of `rank` in `dir` (ascending).");
     m.def("encode_max_key", &encode_max_key);

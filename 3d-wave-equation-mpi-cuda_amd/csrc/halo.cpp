@@ -1,6 +1,8 @@
 #include "halo.hpp"
 
+#include <atomic>
 #include <chrono>
+#include <mutex>
 #include <cstdlib>
 #include <thread>
 
@@ -14,6 +16,51 @@ double watchdog_limit_s() {
     return limit;
 }
 
+namespace {
+std::mutex g_abort_mu;
+std::atomic<bool> g_abort{false};
+std::string g_abort_why;
+}  // namespace
+
+void raise_job_abort(const std::string& why) {
+    std::lock_guard<std::mutex> g(g_abort_mu);
+    if (!g_abort.load()) g_abort_why = why;
+    g_abort.store(true);
+}
+
+bool job_aborted(std::string* why) {
+    if (!g_abort.load(std::memory_order_relaxed)) return false;
+    if (why) {
+        std::lock_guard<std::mutex> g(g_abort_mu);
+        *why = g_abort_why;
+    }
+    return true;
+}
+
+void clear_job_abort() {
+    std::lock_guard<std::mutex> g(g_abort_mu);
+    g_abort.store(false);
+    g_abort_why.clear();
+}
+
+std::vector<std::string> run_rank_threads(int n, const std::function<void(int)>& body) {
+    clear_job_abort();
+    std::vector<std::string> errs(n);
+    std::vector<std::thread> th;
+    for (int r = 0; r < n; ++r)
+        th.emplace_back([&, r] {
+            try {
+                body(r);
+            } catch (const std::exception& e) {
+                errs[r] = e.what();
+                raise_job_abort("rank " + std::to_string(r) + ": " + e.what());
+            }
+        });
+    for (auto& t : th) t.join();
+    clear_job_abort();
+    return errs;
+}
+
 void watch_until(const std::function<bool()>& done, const std::function<std::string()>& async_error,
                  const std::function<long()>* progress, double limit_s,
                  const std::function<void()>& abort, const std::string& what) {
@@ -22,6 +69,11 @@ void watch_until(const std::function<bool()>& done, const std::function<std::str
     long seen = progress ? (*progress)() : 0;
     for (int spin = 0;; ++spin) {
         if (done()) return;
+        std::string why;
+        if (job_aborted(&why)) {
+            abort();
+            throw Error(what + " aborted: another rank failed (" + why + ")");
+        }
         const std::string err = async_error();
         const auto now = clk::now();
         if (progress && (spin & 63) == 0) {

@@ -61,6 +61,19 @@ void watch_until(const std::function<bool()>& done, const std::function<std::str
 // WAVE3D_WATCHDOG_S, default 120 s (below the benchmark driver's timeout)
 double watchdog_limit_s();
 
+// Job-wide abort flag of one process (thread-per-GPU ranks): the first rank thread that fails
+// raises it, and every watch_until() loop of the other ranks — waits on RCCL streams and
+// communicator initialisation — aborts its communicator and throws within a poll interval
+// instead of sitting in a collective until the watchdog limit.
+void raise_job_abort(const std::string& why);
+bool job_aborted(std::string* why = nullptr);
+void clear_job_abort();  // before a new job in the same process (tests)
+
+// Runs body(r) for r = 0..n-1 on n threads (thread-per-GPU ranks) and returns each rank's
+// error message ("" = success). A rank that throws raises the job abort flag, so ranks blocked
+// in watch_until() on it fail within a poll interval. The flag is cleared before and after.
+std::vector<std::string> run_rank_threads(int n, const std::function<void(int)>& body);
+
 // A transport moves the messages of one exchange. Device transports order the operation
 // on `stream` (a hipStream_t) and return without host synchronisation; host transports
 // complete before returning.

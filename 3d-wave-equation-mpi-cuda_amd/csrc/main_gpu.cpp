@@ -75,28 +75,24 @@ int main(int argc, char** argv) {
                                           " present (use --ranks P to simulate ranks on one GPU)");
             std::string id = rccl_unique_id();
             std::vector<RunResult> res(c.Np);
-            std::vector<std::string> errs(c.Np);
-            std::vector<std::thread> th;
             std::mutex io;
-            for (int r = 0; r < c.Np; ++r)
-                th.emplace_back([&, r] {
-                    try {
-                        Config cr = c;
-                        cr.device = r;
-                        if (hipSetDevice(r) != hipSuccess) throw Error("hipSetDevice failed");
-                        if (!c.quiet) {
-                            std::lock_guard<std::mutex> g(io);
-                            std::cout << "Process " << r << " local rank = " << r
-                                      << " local size = " << c.Np << " hostname = " << host_name()
-                                      << " device = " << r << std::endl;
-                        }
-                        RcclTransport tr(r, c.Np, id, r);
-                        res[r] = run_hip(cr, &tr);
-                    } catch (const std::exception& e) {
-                        errs[r] = e.what();
-                    }
-                });
-            for (auto& t : th) t.join();
+            // a failing rank thread raises the job abort flag: the others' RCCL waits return
+            // at once (run_rank_threads, halo.cpp) instead of waiting for the watchdog
+            const std::vector<std::string> errs = run_rank_threads(c.Np, [&](int r) {
+                Config cr = c;
+                cr.device = r;
+                if (hipSetDevice(r) != hipSuccess) throw Error("hipSetDevice failed");
+                if (!c.quiet) {
+                    std::lock_guard<std::mutex> g(io);
+                    std::cout << "Process " << r << " local rank = " << r << " local size = " << c.Np
+                              << " hostname = " << host_name() << " device = " << r << std::endl;
+                }
+                RcclTransport tr(r, c.Np, id, r);
+                res[r] = run_hip(cr, &tr);
+            });
+            for (int r = 0; r < c.Np; ++r)  // the first failure is the cause, the rest followed it
+                if (!errs[r].empty() && errs[r].find("another rank failed") == std::string::npos)
+                    throw Error("rank " + std::to_string(r) + ": " + errs[r]);
             for (int r = 0; r < c.Np; ++r)
                 if (!errs[r].empty()) throw Error("rank " + std::to_string(r) + ": " + errs[r]);
             finish(c, res[0], true);

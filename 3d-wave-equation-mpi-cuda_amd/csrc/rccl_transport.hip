@@ -9,6 +9,7 @@
 #include <sys/socket.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <chrono>
 #include <cstdlib>
 #include <cstring>
@@ -45,34 +46,109 @@ struct RcclTransport::Impl {
     hipStream_t side = nullptr;   // for host-value collectives
     double* scratch = nullptr;    // device scratch for allreduce_max_host
     size_t scratch_n = 0;
+    int max_ctas = 0;             // configured CTA budget (0 = RCCL default)
 };
 
+int RcclTransport::max_ctas() const { return impl_->max_ctas; }
+
+namespace {
+int env_int(const char* k, int dflt) {
+    const char* v = std::getenv(k);
+    return v && *v ? std::atoi(v) : dflt;
+}
+}  // namespace
+
+int rccl_max_ctas() { return env_int("WAVE3D_RCCL_MAX_CTAS", kRcclDefaultMaxCtas); }
+
+// The communicator is non-blocking (config.blocking = 0): initialisation and every enqueue
+// may return ncclInProgress, and settle() polls ncclCommGetAsyncError under the watchdog, so a
+// peer that never arrives at ncclCommInitRank, or a failed rank thread of this process (job
+// abort flag), ends the wait with an error instead of a hang. The CTA budget (maxCTAs,
+// WAVE3D_RCCL_MAX_CTAS) caps how many CUs the halo kernels take from the interior sweep
+// that runs concurrently: a face of a few MB needs a few channels, not RCCL's default.
 RcclTransport::RcclTransport(int rank, int size, const std::string& uid, int device)
     : impl_(new Impl), rank_(rank), size_(size) {
     W3D_REQUIRE(uid.size() == sizeof(ncclUniqueId), "bad RCCL unique id");
     HIP_CHECK_T(hipSetDevice(device));
     ncclUniqueId id;
     std::memcpy(&id, uid.data(), sizeof(id));
-    NCCL_CHECK(ncclCommInitRank(&impl_->comm, size, id, rank));
+    ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+    cfg.blocking = 0;
+    const int mx = rccl_max_ctas();
+    if (mx > 0) {
+        cfg.maxCTAs = mx;
+        cfg.minCTAs = std::min(mx, env_int("WAVE3D_RCCL_MIN_CTAS", 1));
+    }
+    impl_->max_ctas = mx;
+    const ncclResult_t r = ncclCommInitRankConfig(&impl_->comm, size, id, rank, &cfg);
+    if (r != ncclSuccess && r != ncclInProgress) {
+        if (impl_->comm) (void)ncclCommAbort(impl_->comm);
+        impl_->comm = nullptr;
+        NCCL_CHECK(r);
+    }
+    settle(r, init_limit_s(), "RCCL init");
     HIP_CHECK_T(hipStreamCreateWithFlags(&impl_->side, hipStreamNonBlocking));
+}
+
+double RcclTransport::init_limit_s() {
+    const char* e = std::getenv("WAVE3D_RCCL_INIT_S");
+    return e ? std::atof(e) : 120.0;
+}
+
+// ncclInProgress: poll until the communicator's state leaves it (watchdog, job abort)
+void RcclTransport::settle(int r0, double limit_s, const char* what) {
+    ncclResult_t r = ncclResult_t(r0);
+    if (r == ncclSuccess) return;
+    if (r != ncclInProgress) NCCL_CHECK(r);
+    W3D_REQUIRE(impl_->comm, "RCCL communicator missing");
+    ncclResult_t st = ncclInProgress;
+    watch_until(
+        [&] {
+            NCCL_CHECK(ncclCommGetAsyncError(impl_->comm, &st));
+            return st != ncclInProgress;
+        },
+        [&] { return st == ncclSuccess || st == ncclInProgress ? std::string() : std::string(ncclGetErrorString(st)); },
+        nullptr, limit_s,
+        [&] {
+            (void)ncclCommAbort(impl_->comm);
+            impl_->comm = nullptr;
+        },
+        what);
+    if (st != ncclSuccess) {
+        (void)ncclCommAbort(impl_->comm);
+        impl_->comm = nullptr;
+        throw Error(std::string(what) + " failed: " + ncclGetErrorString(st));
+    }
 }
 
 RcclTransport::~RcclTransport() {
     if (impl_->scratch) (void)hipFree(impl_->scratch);
     if (impl_->side) (void)hipStreamDestroy(impl_->side);
-    if (impl_->comm) (void)ncclCommDestroy(impl_->comm);
+    if (!impl_->comm) return;
+    // non-blocking communicator: finalize (flushes outstanding work), wait for it, destroy;
+    // any failure or a stuck finalize falls back to abort
+    ncclResult_t r = ncclCommFinalize(impl_->comm), st = r;
+    const auto t0 = std::chrono::steady_clock::now();
+    while (r == ncclInProgress || r == ncclSuccess) {
+        if (ncclCommGetAsyncError(impl_->comm, &st) != ncclSuccess || st != ncclInProgress) break;
+        if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(30)) break;
+        std::this_thread::sleep_for(std::chrono::microseconds(200));
+    }
+    if ((r == ncclSuccess || r == ncclInProgress) && st == ncclSuccess) (void)ncclCommDestroy(impl_->comm);
+    else (void)ncclCommAbort(impl_->comm);
 }
 
 void RcclTransport::exchange(const std::vector<Message>& sends, const std::vector<Message>& recvs,
                              void* stream) {
     TraceRange tr("rccl.exchange");
     hipStream_t s = static_cast<hipStream_t>(stream);
+    W3D_REQUIRE(impl_->comm, "RCCL communicator was aborted");
     NCCL_CHECK(ncclGroupStart());
     for (const auto& m : sends)
         NCCL_CHECK(ncclSend(m.ptr, m.bytes, ncclChar, m.peer, impl_->comm, s));
     for (const auto& m : recvs)
         NCCL_CHECK(ncclRecv(m.ptr, m.bytes, ncclChar, m.peer, impl_->comm, s));
-    NCCL_CHECK(ncclGroupEnd());
+    settle(ncclGroupEnd(), watchdog_limit_s(), "RCCL group");
 }
 
 int RcclTransport::comm_size() const {
@@ -83,8 +159,9 @@ int RcclTransport::comm_size() const {
 }
 
 void RcclTransport::allreduce_max_u64(u64* data, size_t n, void* stream) {
-    NCCL_CHECK(ncclAllReduce(data, data, n, ncclUint64, ncclMax, impl_->comm,
-                             static_cast<hipStream_t>(stream)));
+    W3D_REQUIRE(impl_->comm, "RCCL communicator was aborted");
+    settle(ncclAllReduce(data, data, n, ncclUint64, ncclMax, impl_->comm, static_cast<hipStream_t>(stream)),
+           watchdog_limit_s(), "RCCL allreduce");
 }
 
 void RcclTransport::allreduce_max_host(double* data, size_t n) {
@@ -95,8 +172,9 @@ void RcclTransport::allreduce_max_host(double* data, size_t n) {
     }
     HIP_CHECK_T(hipMemcpyAsync(impl_->scratch, data, n * sizeof(double), hipMemcpyHostToDevice,
                                impl_->side));
-    NCCL_CHECK(ncclAllReduce(impl_->scratch, impl_->scratch, n, ncclFloat64, ncclMax, impl_->comm,
-                             impl_->side));
+    W3D_REQUIRE(impl_->comm, "RCCL communicator was aborted");
+    settle(ncclAllReduce(impl_->scratch, impl_->scratch, n, ncclFloat64, ncclMax, impl_->comm, impl_->side),
+           watchdog_limit_s(), "RCCL allreduce");
     HIP_CHECK_T(hipMemcpyAsync(data, impl_->scratch, n * sizeof(double), hipMemcpyDeviceToHost,
                                impl_->side));
     wait_stream(impl_->side);
@@ -108,6 +186,7 @@ void RcclTransport::barrier() {
 }
 
 void RcclTransport::check_async() const {
+    W3D_REQUIRE(impl_->comm, "RCCL communicator was aborted");
     ncclResult_t st = ncclSuccess;
     NCCL_CHECK(ncclCommGetAsyncError(impl_->comm, &st));
     if (st != ncclSuccess) throw Error(std::string("RCCL async error: ") + ncclGetErrorString(st));
@@ -123,12 +202,13 @@ bool RcclTransport::wait_stream(void* stream, const std::function<long()>* progr
         },
         [&] {
             ncclResult_t st = ncclSuccess;
+            if (!impl_->comm) return std::string("communicator aborted");
             NCCL_CHECK(ncclCommGetAsyncError(impl_->comm, &st));
-            return st == ncclSuccess ? std::string() : std::string(ncclGetErrorString(st));
+            return st == ncclSuccess || st == ncclInProgress ? std::string() : std::string(ncclGetErrorString(st));
         },
         progress, watchdog_limit_s(),
         [&] {
-            (void)ncclCommAbort(impl_->comm);
+            if (impl_->comm) (void)ncclCommAbort(impl_->comm);
             impl_->comm = nullptr;
         },
         "RCCL");

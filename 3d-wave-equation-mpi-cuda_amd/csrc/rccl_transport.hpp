@@ -17,6 +17,11 @@ constexpr int kRcclIdBytes = 128;  // sizeof(ncclUniqueId)
 
 std::string rccl_unique_id();  // 128 raw bytes
 
+// CTA budget of the halo communicator: WAVE3D_RCCL_MAX_CTAS, default kRcclDefaultMaxCtas
+// (<= 0: RCCL's own default)
+constexpr int kRcclDefaultMaxCtas = 8;
+int rccl_max_ctas();
+
 class RcclTransport : public Transport {
 public:
     // Must be called with `device` as the current device on this thread.
@@ -39,8 +44,11 @@ public:
     // without progress — measured from the last growth of `progress` when given — so a dead
     // peer ends the run with an error instead of a hang.
     bool wait_stream(void* stream, const std::function<long()>* progress = nullptr) override;
+    int max_ctas() const;  // CTA budget the communicator was created with (0 = RCCL default)
+    static double init_limit_s();  // WAVE3D_RCCL_INIT_S, default 120 s
 
 private:
+    void settle(int nccl_result, double limit_s, const char* what);
     struct Impl;
     std::unique_ptr<Impl> impl_;
     int rank_, size_;

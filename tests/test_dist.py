@@ -114,3 +114,17 @@ def test_watchdog_is_progress_based(C):
     # progress stalls at 0.1 s, never done: aborted ~0.3 s later
     with pytest.raises(Exception, match="no progress"):
         C.watchdog_probe(0.3, 100.0, 0.1)
+
+
+def test_thread_ranks_fail_fast(C):
+    """Thread-per-GPU ranks (`wave3d N 8 ...`): when one rank thread throws, the others — blocked
+    in the RCCL watchdog loop, here with a 60 s limit — see the job abort flag and fail within a
+    poll interval, naming the failed rank, instead of waiting out the watchdog."""
+    out = C.abort_probe(4, 1, 0.2, 60.0)
+    assert out[1][1] == "injected failure"
+    for r in (0, 2, 3):
+        t, err = out[r]
+        assert "another rank failed" in err and "rank 1: injected failure" in err
+        assert 0.15 < t < 5.0
+    # the flag is cleared when the job ends: a later wait is unaffected
+    assert 0.2 < C.watchdog_probe(5.0, 0.25, 0.25) < 2.0
