@@ -94,8 +94,11 @@ py::dict result_dict(const Config& c, const RunResult& r) {
     d["resumed_from"] = r.resumed_from;
     d["graph"] = r.graph;
     d["overlap"] = r.overlap;
+    d["overlap_mode"] = r.overlap_mode;
+    d["overlap_trial_ms"] = py::make_tuple(r.overlap_trial_ms[0], r.overlap_trial_ms[1]);
     d["comm_size"] = r.comm_size;
     d["halo_checked"] = r.halo_checked;
+    d["rccl_mirror_msgs"] = r.rccl_mirror_msgs;
     d["report"] = format_report(c, r);
     d["output_file"] = output_filename(c, r);
     d["json"] = json_summary(c, r);
@@ -358,6 +361,7 @@ PYBIND11_MODULE(_wave3d_C, m) {
         d["hx"] = p.hx, d["hy"] = p.hy, d["hz"] = p.hz;
         d["coef"] = p.coef, d["coef_first"] = p.coef_first, d["courant"] = p.courant;
         d["dtype"] = dtype_name(c.dtype), d["ranks"] = c.ranks, d["overlap"] = c.overlap;
+        d["overlap_auto"] = c.overlap_auto, d["rccl_mirror"] = c.rccl_mirror, d["halo_check"] = c.halo_check;
         d["kernel"] = c.kernel, d["chunk"] = c.chunk;
         d["dims"] = std::vector<int>{c.dims[0], c.dims[1], c.dims[2]};
         d["table_x"] = p.table_x(), d["table_y"] = p.table_y(), d["table_z"] = p.table_z();

@@ -18,7 +18,9 @@ std::string usage() {
            "  --transport auto|rccl|loopback\n"
            "  --x-self-transport     one x rank: send the periodic wrap through the transport\n"
            "                         to this rank (exercises RCCL send/recv on a single GPU)\n"
-           "  --no-overlap           no interior/shell split\n"
+           "  --overlap auto|on|off  interior/shell split with the halo on a second stream; auto\n"
+           "                         (default) times the first two solves on / off, keeps the faster\n"
+           "  --no-overlap           = --overlap off\n"
            "  --kernel K             auto (= tb2) | tb2[r<R>][w<W>] | tb3[r<R>w<W>] | march[2|4|8][nt|p|f]\n"
            "                         | naive | flat   (temporal blocking / single-step variants)\n"
            "  --chunk C              i-planes per marching work item\n"
@@ -35,6 +37,8 @@ std::string usage() {
            "  --dump PATH            write the final layer u^K as float64 .npy\n"
            "  --fault SPEC           fault injection (drop_face:RANK:LAYER | nan:RANK:LAYER |\n"
            "                         corrupt_tag:RANK:TAG = halo self-test delivery of TAG to RANK)\n"
+           "  --rccl-mirror          with --ranks P: also send every halo message (and the error\n"
+           "                         allreduce) through a 1-rank RCCL communicator, compare bitwise\n"
            "  --no-halo-check        skip the init-time halo self-test (patterns through the real plan)\n"
            "  --device d  --threads t  --print-layers  --quiet\n";
 }
@@ -136,8 +140,13 @@ Config parse_cli(const std::vector<std::string>& a) {
             c.x_self_transport = true;
         } else if (o == "--no-overlap") {
             c.overlap = false;
+            c.overlap_auto = false;
         } else if (o == "--overlap") {
-            c.overlap = true;
+            // --overlap [on|off|auto]; bare --overlap = on
+            std::string v = "on";
+            if (i + 1 < a.size() && (a[i + 1] == "on" || a[i + 1] == "off" || a[i + 1] == "auto")) v = a[++i];
+            c.overlap = v != "off";
+            c.overlap_auto = v == "auto";
         } else if (o == "--kernel") {
             c.kernel = need(i++);
         } else if (o == "--chunk") {
@@ -182,6 +191,8 @@ Config parse_cli(const std::vector<std::string>& a) {
             else if (v == "off") c.graph = 0;
             else if (v == "auto") c.graph = -1;
             else throw Error("--graph must be on, off or auto");
+        } else if (o == "--rccl-mirror") {
+            c.rccl_mirror = true;
         } else if (o == "--no-halo-check") {
             c.halo_check = false;
         } else if (o == "--fault") {

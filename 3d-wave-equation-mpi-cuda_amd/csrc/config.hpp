@@ -34,6 +34,8 @@ struct Config {
     ICMode ic = ICMode::Ref;
     int dims[3] = {0, 0, 0};        // 0 = let dims_create choose (MPI_Dims_create semantics)
     bool overlap = true;            // interior/shell split with comm on a second stream
+    bool overlap_auto = true;       // --overlap auto (default): the first two solves with halos
+                                    // run overlap on, then off; the faster arm is kept
     bool json = false;              // one-line JSON summary on stdout (rank 0)
     int check_every = 0;            // >0: abort early when a layer's error is NaN/Inf/>1
     bool strict_cfl = false;        // refuse C > 1/sqrt(3)
@@ -42,6 +44,8 @@ struct Config {
                                     // x wrap travels as messages to this rank (RCCL self
                                     // send/recv) instead of the fused local wrap (testing)
     int ranks = 0;                  // >0: number of logical ranks simulated in-process
+    bool rccl_mirror = false;       // --ranks P: every loopback halo message also through a
+                                    // 1-rank RCCL communicator, compared bitwise (testing)
     ReportFormat format = ReportFormat::New;
     std::string out_dir = ".";
     std::string out_name;           // override of output_N{N}_Np{Np}.txt

@@ -22,6 +22,7 @@
 #include "checkpoint.hpp"
 #include "hip_kernels.hpp"
 #include "hip_selftest.hpp"
+#include "rccl_transport.hpp"
 #include "problem.hpp"
 #include "sizing.hpp"
 #include "solver.hpp"
@@ -150,10 +151,12 @@ public:
         }
         // interior/shell split + comm stream whenever there is a remote halo to hide
         overlap_ = c.overlap && (ext_ != nullptr || world_ > 1);
+        overlap_auto_ = overlap_ && c.overlap_auto;
         // test mode: the periodic x wrap of a dims[0] == 1 rank goes through the transport as
         // messages to itself (RCCL send/recv exercised on one GPU), not the fused local wrap
         xself_ = c.x_self_transport;
         W3D_REQUIRE(!xself_ || ext_, "--x-self-transport needs an external (e.g. RCCL) transport");
+        W3D_REQUIRE(!c.rccl_mirror || (!ext_ && world_ > 1), "--rccl-mirror needs simulated ranks (--ranks P)");
     }
 
     ~HipSolver() { release(); }
@@ -162,6 +165,7 @@ public:
         TraceRange tr("wave3d.setup");
         auto t0 = clk::now();
         setup();
+        if (cfg_.rccl_mirror) setup_mirror();
         bool msgs = false;
         for (auto& R : ranks_) msgs |= !R.plan.sends.empty() || !R.plan.recvs.empty() || tb_halo(R);
         if (msgs && cfg_.halo_check) halo_self_test();
@@ -210,7 +214,15 @@ public:
         res.kernel = tb_ ? tb_name(tb_rows_, tb_waves_, tb_occ_, tbd_, tb_nwk_) : kernel_variant_name(kind_);
         res.courant = prob_.courant;
         res.transport = ext_ ? ext_->name() : (world_ > 1 ? "loopback" : "self");
+        // --overlap auto: the first two solves are the trials (on, then off); the arm with the
+        // shorter max-over-ranks solve time is kept for every later solve — the same decision
+        // on every rank, since the times are reduced before the comparison
+        const int trial = overlap_auto_ && trials_done_ < 2 ? trials_done_ : -1;
+        if (trial >= 0) set_overlap(trial == 0);
         res.overlap = overlap_;
+        res.overlap_mode = !(ext_ || world_ > 1) ? "none"
+                           : overlap_auto_       ? "auto"
+                           : (overlap_ ? "on" : "off");
         res.scheme = cfg_.delta ? "delta" : "leapfrog";
         res.comm_size = ext_ ? ext_->comm_size() : 0;
         res.halo_checked = halo_checked_;
@@ -222,6 +234,15 @@ public:
         if (ext_) ext_->allreduce_max_host(tv, 5);
         t.total_ms = tv[0], t.loop_ms = tv[1], t.exchange_ms = tv[2], t.comm_ms = tv[3];
         t.error_ms = tv[4];
+        if (trial >= 0) {
+            trial_ms_[trial] = t.total_ms;
+            if (++trials_done_ == 2) {
+                set_overlap(trial_ms_[0] <= trial_ms_[1]);
+                log_msg(LogLevel::Info, "overlap auto: on ", trial_ms_[0], " ms, off ", trial_ms_[1], " ms -> ",
+                        overlap_ ? "on" : "off");
+            }
+        }
+        res.overlap_trial_ms[0] = trial_ms_[0], res.overlap_trial_ms[1] = trial_ms_[1];
         res.t = t;
         res.solve_ms.push_back(t.total_ms);
         return res;
@@ -431,6 +452,10 @@ private:
             }
         }
         ranks_.clear();
+        if (mirror_buf_) (void)hipFree(mirror_buf_);
+        if (mirror_res_) (void)hipFree(mirror_res_);
+        mirror_buf_ = nullptr, mirror_res_ = nullptr;
+        mirror_.reset();
         if (s_comp_) (void)hipStreamDestroy(s_comp_);
         if (s_comm_) (void)hipStreamDestroy(s_comm_);
         for (auto e : {ev_start_, ev_end_, ev_layer_, ev_halo_, ev_shell_})
@@ -443,6 +468,13 @@ private:
     }
 
     // ---- helpers ----------------------------------------------------------------------
+    // the enqueue order depends on overlap_: a captured graph of the other arm is dropped
+    void set_overlap(bool on) {
+        if (on == overlap_) return;
+        overlap_ = on;
+        if (gexec_) (void)hipGraphExecDestroy(gexec_);
+        gexec_ = nullptr;
+    }
     // start of the contiguous block of logical plane i (all rows, ghosts included)
     T* plane(DevRank<T>& R, int level, int i) {
         return R.g[level] + i64(i) * R.gv.si - R.plane_off;
@@ -656,9 +688,8 @@ private:
                     for (auto& g : D.tb_recvs)
                         if (g.peer == S.topo.rank && g.tag == m.tag) {
                             W3D_REQUIRE(g.nplanes == m.nplanes, "tb halo size mismatch");
-                            HIP_CHECK(hipMemcpyAsync(tb_ptr(D, g, mD), tb_ptr(S, m, mD),
-                                                     size_t(m.nplanes) * S.gv.si * sizeof(T),
-                                                     hipMemcpyDeviceToDevice, s));
+                            loop_copy(tb_ptr(D, g, mD), tb_ptr(S, m, mD), size_t(m.nplanes) * S.gv.si * sizeof(T),
+                                      S.topo.rank, D.topo.rank, m.tag, s);
                             done = true;
                             break;
                         }
@@ -704,8 +735,7 @@ private:
                         for (auto& g : ranks_[m.peer].tb_brecvs[rd])
                             if (g.peer == S.topo.rank && g.tag == m.tag) {
                                 W3D_REQUIRE(bytes(g) == bytes(m), "tb box halo size mismatch");
-                                HIP_CHECK(hipMemcpyAsync(g.buf, m.buf, bytes(m),
-                                                         hipMemcpyDeviceToDevice, s));
+                                loop_copy(g.buf, m.buf, bytes(m), S.topo.rank, m.peer, m.tag, s);
                                 done = true;
                                 break;
                             }
@@ -857,8 +887,8 @@ private:
                     const auto& g = D.plan.recvs[q];
                     if (g.peer == S.topo.rank && g.tag == f.tag) {
                         W3D_REQUIRE(g.count == f.count, "halo size mismatch");
-                        HIP_CHECK(hipMemcpyAsync(recv_ptr(D, q, n), send_ptr(S, m, n),
-                                                 f.count * sizeof(T), hipMemcpyDeviceToDevice, s));
+                        loop_copy(recv_ptr(D, q, n), send_ptr(S, m, n), f.count * sizeof(T), S.topo.rank,
+                                  D.topo.rank, f.tag, s);
                         done = true;
                         break;
                     }
@@ -869,6 +899,74 @@ private:
             pack_faces(R, n, s, false);
             inject_after_exchange(R, n, s);
         }
+    }
+
+    // ---- loopback copies and the RCCL mirror ------------------------------------------------
+    // One halo message between two in-process ranks: a D2D copy. With --rccl-mirror every such
+    // message also travels through a 1-rank RCCL communicator (ncclSend/ncclRecv to itself, the
+    // same group call, bytes and stream order as a real multi-GPU rank) into a scratch buffer,
+    // and a device compare against the loopback copy counts differing words per message kind:
+    // every message shape of the multi-GPU plan runs through RCCL on one GPU, bit for bit.
+    void loop_copy(void* dst, const void* src, size_t bytes, int src_rank, int dst_rank, int tag, hipStream_t s) {
+        HIP_CHECK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, s));
+        if (!mirror_) return;
+        W3D_REQUIRE(bytes <= mirror_bytes_, "rccl mirror scratch too small");
+        mirror_->exchange({Message{0, tag, const_cast<void*>(src), bytes}}, {Message{0, tag, mirror_buf_, bytes}}, s);
+        launch_compare_bytes(mirror_buf_, dst, bytes, mirror_res_ + 2 * mirror_slot(src_rank, dst_rank, tag), s);
+        ++mirror_msgs_;
+    }
+
+    int mirror_slot(int src, int dst, int tag) {
+        const std::string key = "rank " + std::to_string(src) + " -> rank " + std::to_string(dst) + " tag " +
+                                std::to_string(tag);
+        for (size_t q = 0; q < mirror_keys_.size(); ++q)
+            if (mirror_keys_[q] == key) return int(q);
+        W3D_REQUIRE(mirror_keys_.size() < kMirrorSlots, "too many distinct halo messages for the rccl mirror");
+        mirror_keys_.push_back(key);
+        return int(mirror_keys_.size()) - 1;
+    }
+
+    void setup_mirror() {
+        size_t most = 8 * (size_t(prob_.K) + 1) * kSlotsPerLayer;  // the error-key allreduce
+        for (auto& R : ranks_) {
+            for (auto& f : R.plan.sends) most = std::max(most, size_t(f.count) * sizeof(T));
+            for (auto& m : R.tb_sends) most = std::max(most, size_t(m.nplanes) * size_t(R.gv.si) * sizeof(T));
+            for (int rd = 0; rd < 2; ++rd)
+                for (auto& m : R.tb_bsends[rd]) most = std::max(most, size_t(m.box.count()) * sizeof(T));
+        }
+        int dev = 0;
+        HIP_CHECK(hipGetDevice(&dev));
+        mirror_ = std::make_unique<RcclTransport>(0, 1, rccl_unique_id(), dev);
+        mirror_bytes_ = most;
+        HIP_CHECK(hipMalloc(&mirror_buf_, most));
+        HIP_CHECK(hipMalloc(&mirror_res_, sizeof(u64) * 2 * kMirrorSlots));
+        reset_mirror();
+    }
+
+    void reset_mirror() {
+        std::vector<u64> init(2 * kMirrorSlots);
+        for (size_t q = 0; q < init.size(); ++q) init[q] = q % 2 ? ~0ull : 0ull;
+        HIP_CHECK(hipMemcpy(mirror_res_, init.data(), init.size() * sizeof(u64), hipMemcpyHostToDevice));
+    }
+
+    // after a solve: the error keys through a 1-rank ncclAllReduce(max) too, then every count
+    void check_mirror(const u64* err, size_t n, hipStream_t s) {
+        HIP_CHECK(hipMemcpyAsync(mirror_buf_, err, n * sizeof(u64), hipMemcpyDeviceToDevice, s));
+        mirror_->allreduce_max_u64(static_cast<u64*>(mirror_buf_), n, s);
+        launch_compare_bytes(mirror_buf_, err, n * sizeof(u64), mirror_res_ + 2 * mirror_slot(0, 0, -1), s);
+        ++mirror_msgs_;
+        std::vector<u64> res(2 * kMirrorSlots);
+        HIP_CHECK(hipMemcpyAsync(res.data(), mirror_res_, res.size() * sizeof(u64), hipMemcpyDeviceToHost, s));
+        sync(s);
+        std::string bad;
+        for (size_t q = 0; q < mirror_keys_.size(); ++q)
+            if (res[2 * q])
+                bad += "\n  " + (mirror_keys_[q] == "rank 0 -> rank 0 tag -1" ? std::string("error-key allreduce")
+                                                                            : mirror_keys_[q]) +
+                       ": " + std::to_string(res[2 * q]) + " words differ (first word " +
+                       std::to_string(res[2 * q + 1]) + ")";
+        reset_mirror();
+        if (!bad.empty()) throw Error("wave3d: RCCL mirror differs from the loopback copies:" + bad);
     }
 
     // ---- init-time halo self-test ---------------------------------------------------------
@@ -1119,6 +1217,7 @@ private:
         }
         mark(s_comp_, 5, kAlways);
         HIP_CHECK(hipEventRecord(ev_end_, s_comp_));
+        if (mirror_) check_mirror(ranks_[0].err, nslot, s_comp_);  // outside the timed interval
         HIP_CHECK(hipEventSynchronize(ev_end_));
         finish_checkpoint();  // files complete when solve() returns
         float ms = 0;
@@ -1134,6 +1233,7 @@ private:
             for (int n = 0; n <= res.resumed_from && n < int(ckpt_abs_.size()); ++n)
                 res.max_abs[n] = ckpt_abs_[n], res.max_rel[n] = ckpt_rel_[n];
         collect_profile(tm);
+        res.rccl_mirror_msgs = mirror_msgs_;
     }
 
     // ---- time loop ----------------------------------------------------------------------
@@ -1253,7 +1353,7 @@ private:
     // interaction inside the loop (no external transport, checks, checkpoints, profiling,
     // faults); a failed capture falls back to direct launches.
     bool graph_eligible() const {
-        return cfg_.graph != 0 && !ext_ && cfg_.check_every == 0 && cfg_.checkpoint_every == 0 &&
+        return cfg_.graph != 0 && !ext_ && !mirror_ && cfg_.check_every == 0 && cfg_.checkpoint_every == 0 &&
                cfg_.resume_dir.empty() && fault_.kind.empty() &&
                !cfg_.print_layers;
     }
@@ -1533,7 +1633,17 @@ private:
     int G_ = 1;         // ghost depth
     int L_ = 3;         // time levels kept
     bool overlap_ = false;
+    bool overlap_auto_ = false;   // --overlap auto with a remote halo
+    int trials_done_ = 0;         // overlap auto trials run (on, off)
+    double trial_ms_[2] = {0, 0};
     bool xself_ = false;  // --x-self-transport
+    static constexpr size_t kMirrorSlots = 64;
+    std::unique_ptr<RcclTransport> mirror_;  // --rccl-mirror: 1-rank communicator
+    void* mirror_buf_ = nullptr;
+    size_t mirror_bytes_ = 0;
+    u64* mirror_res_ = nullptr;              // per message kind: differing words, first word
+    std::vector<std::string> mirror_keys_;
+    long mirror_msgs_ = 0;                   // messages mirrored (all solves)
     bool selftest_ = false;  // inside halo_self_test()
     int halo_checked_ = 0;   // messages verified by the init-time halo self-test
     int world_ = 1;

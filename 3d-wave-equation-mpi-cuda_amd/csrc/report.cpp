@@ -93,8 +93,10 @@ std::string json_summary(const Config& c, const RunResult& r) {
       << ", \"dtype\": \"" << dtype_name(r.dtype) << "\", \"backend\": \"" << r.backend
       << "\", \"kernel\": \"" << r.kernel << "\", \"scheme\": \"" << r.scheme
       << "\", \"transport\": \"" << r.transport << "\""
-      << ", \"overlap\": " << (r.overlap ? "true" : "false")
+      << ", \"overlap\": " << (r.overlap ? "true" : "false") << ", \"overlap_mode\": \"" << r.overlap_mode
+      << "\", \"overlap_trial_ms\": [" << jnum(r.overlap_trial_ms[0]) << ", " << jnum(r.overlap_trial_ms[1]) << "]"
       << ", \"comm_size\": " << r.comm_size << ", \"halo_checked\": " << r.halo_checked
+      << ", \"rccl_mirror_msgs\": " << r.rccl_mirror_msgs
       << ", \"courant\": " << jnum(r.courant) << ", \"total_ms\": " << jnum(r.t.total_ms)
       << ", \"init_ms\": " << jnum(r.t.init_ms) << ", \"loop_ms\": " << jnum(r.t.loop_ms)
       << ", \"exchange_ms\": " << jnum(r.t.exchange_ms) << ", \"comm_ms\": " << jnum(r.t.comm_ms)

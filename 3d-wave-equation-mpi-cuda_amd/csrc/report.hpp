@@ -38,7 +38,10 @@ struct RunResult {
     int resumed_from = -1;
     bool graph = false;  // time loop replayed as one hipGraph
     bool overlap = false;  // interior/shell split with the halo on a second stream (effective)
+    std::string overlap_mode = "off";  // "on" | "off" | "auto" (requested; "none" = no halo)
+    double overlap_trial_ms[2] = {0, 0};  // --overlap auto: solve time with overlap on / off
     int comm_size = 0;     // ranks the transport's communicator reports (ncclCommCount), 0 = none
+    long rccl_mirror_msgs = 0;  // --rccl-mirror: messages sent through RCCL and compared
     int halo_checked = 0;  // halo messages verified by the init-time self-test (0 = none ran)
 
     double points() const { return double(N + 1) * double(N + 1) * double(N + 1); }

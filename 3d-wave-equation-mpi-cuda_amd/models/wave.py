@@ -124,13 +124,14 @@ class WaveSolver:
 
     backend   "hip" (MI355X kernels) or "cpu" (OpenMP oracle)
     ranks     >0: simulate that many ranks in this process (loopback transport)
+    overlap   True / False / "auto" (time the first two solves on and off, keep the faster)
     graph     "auto" | "on" | "off": replay the IC + time loop as one hipGraph
     transport a native transport (``parallel.rccl_transport()`` / ``TorchHostTransport``)
               making this process one rank of a distributed job
     """
 
     def __init__(self, problem: WaveProblem, backend: str = "hip", *, ranks: int = 0,
-                 dims=None, overlap: bool = True, kernel: str = "auto", chunk: int = 0,
+                 dims=None, overlap=True, kernel: str = "auto", chunk: int = 0,
                  transport=None, Np: int | None = None, threads: int = 0, fmt: str = "none",
                  out_dir: str | None = None, check_every: int = 0, fault: str | None = None,
                  checkpoint_every: int = 0, checkpoint_dir: str | None = None,
@@ -140,7 +141,8 @@ class WaveSolver:
         self.backend = backend
         self.transport = transport
         self.Np = Np if Np is not None else (transport.size() if transport is not None else max(1, ranks))
-        self.opts = dict(ranks=ranks or None, dims=dims, no_overlap=not overlap, kernel=kernel,
+        ov = overlap if isinstance(overlap, str) else ("on" if overlap else "off")
+        self.opts = dict(ranks=ranks or None, dims=dims, overlap=ov, kernel=kernel,
                          chunk=chunk or None, threads=threads or None, format=fmt,
                          out_dir=out_dir, check_every=check_every or None, fault=fault,
                          checkpoint_every=checkpoint_every or None,

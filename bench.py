@@ -56,7 +56,10 @@ def main() -> int:
     ap.add_argument("--dtype", default="fp64", choices=["fp64", "fp32"])
     ap.add_argument("--kernel", default="auto")
     ap.add_argument("--chunk", type=int, default=0)
-    ap.add_argument("--no-overlap", action="store_true")
+    ap.add_argument("--overlap", default="auto", choices=["auto", "on", "off"],
+                    help="interior/shell split with the halo on a second stream; auto times the first "
+                         "two solves (warmup) on and off and keeps the faster")
+    ap.add_argument("--no-overlap", action="store_true", help="= --overlap off")
     ap.add_argument("--backend", default="hip", choices=["hip", "cpu"])
     ap.add_argument("--profile", action="store_true", help="per-phase timers (slower)")
     ap.add_argument("--transport", default="rccl", choices=["rccl", "staged"],
@@ -144,7 +147,7 @@ def main() -> int:
     if not prob.stable():
         print(f"bench: warning: C={prob.courant:.3f} > 1/sqrt(3) (unstable)", file=sys.stderr)
     solver = wave3d.WaveSolver(prob, a.backend, transport=transport, Np=n_gpus, kernel=a.kernel, dims=dims,
-                               chunk=a.chunk, overlap=not a.no_overlap, profile=a.profile,
+                               chunk=a.chunk, overlap="off" if a.no_overlap else a.overlap, profile=a.profile,
                                device=(torch.cuda.current_device() if a.backend == "hip" else None))
     args = solver.args()
     sess = C.Session(args, a.backend, transport)
@@ -200,6 +203,8 @@ def main() -> int:
             "dims": dims,
             "kernel": res["kernel"],
             "overlap": bool(res["overlap"]),  # effective (off when there is no remote halo)
+            "overlap_mode": res.get("overlap_mode"),
+            "overlap_trial_ms": list(res.get("overlap_trial_ms", (0, 0))),
             "transport": res["transport"],
             "hip_graph": bool(res.get("graph", False)),
             "fill_hbm": a.fill_hbm or None,

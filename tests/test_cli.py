@@ -107,3 +107,17 @@ def test_console_entry_point_runs_the_cpu_program(C, tmp_path, monkeypatch):
     monkeypatch.chdir(tmp_path)
     assert cli.cpu_main(["16", "2", "pi", "pi", "pi", "1", "10", "--quiet"]) == 0
     assert (tmp_path / "output_N16_Np2.txt").exists()
+
+
+@pytest.mark.parametrize("flags,ov,auto", [([], True, True), (["--overlap"], True, False),
+                                           (["--overlap", "on"], True, False), (["--overlap", "off"], False, False),
+                                           (["--overlap", "auto"], True, True), (["--no-overlap"], False, False)])
+def test_overlap_modes(C, flags, ov, auto):
+    d = C.parse(["32", "1", "pi", "pi", "pi"] + flags + ["--kernel", "tb2"])
+    assert (d["overlap"], d["overlap_auto"]) == (ov, auto) and d["kernel"] == "tb2"
+
+
+def test_test_mode_flags(C):
+    d = C.parse(["32", "1", "pi", "pi", "pi", "--rccl-mirror", "--no-halo-check", "--fault", "corrupt_tag:1:11"])
+    assert d["rccl_mirror"] and not d["halo_check"]
+    assert C.parse(["32", "1", "pi", "pi", "pi"])["halo_check"]

@@ -62,3 +62,39 @@ def test_halo_selftest_can_be_skipped(gpu_prog):
     assert out.returncode == 0, out.stderr[-2000:]
     r = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][0])
     assert r["halo_checked"] == 0
+
+
+MIRROR = [("2,2,2", "tb2", "fp64"), ("1,2,2", "tb2", "fp64"), ("2,2,2", "tb3", "fp64"), ("1,2,2", "tb3", "fp32"),
+          ("2,2,2", "march2", "fp64"), ("1,2,2", "march2", "fp64"), ("2,1,1", "tb3", "fp64")]
+
+
+@pytest.mark.parametrize("dims,kernel,dtype", MIRROR)
+@pytest.mark.parametrize("overlap", ["on", "off"])
+def test_rccl_mirror_every_message_shape(gpu_prog, cpu_prog, dims, kernel, dtype, overlap):
+    """--rccl-mirror: every halo message of the multi-GPU plan (x planes, seam alias planes,
+    y/z box rounds, faces) and the error-key allreduce also run through a 1-rank RCCL
+    communicator and are compared bitwise on the device with the loopback copy; the per-layer
+    errors equal the OpenMP oracle's (same decomposition)."""
+    out, _ = _run(gpu_prog, dims, kernel, dtype, ["--rccl-mirror", "--overlap", overlap, "--repeat", "2"])
+    assert out.returncode == 0, out.stderr[-3000:]
+    r = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][0])
+    assert r["rccl_mirror_msgs"] > 0 and r["halo_checked"] > 0 and r["overlap"] == (overlap == "on")
+    P = 1
+    for d in dims.split(","):
+        P *= int(d)
+    ref = subprocess.run([cpu_prog] + ARGS + ["--ranks", str(P), "--dims", dims, "--dtype", dtype, "--json",
+                                              "--quiet", "--format", "none", "--threads", "4"],
+                         capture_output=True, text=True, timeout=120)
+    o = json.loads([l for l in ref.stdout.splitlines() if l.startswith("{")][0])
+    assert r["linf_abs"] == o["linf_abs"] and r["max_rel_final"] == o["max_rel_final"]
+
+
+def test_overlap_auto_trials_then_keeps_the_faster(gpu_prog):
+    """--overlap auto (the default): solve 1 runs overlapped, solve 2 not, later solves use the
+    arm with the shorter (max-over-ranks) time; the JSON records both trial times."""
+    out, _ = _run(gpu_prog, "2,2,2", "tb2", "fp64", ["--repeat", "3"])
+    assert out.returncode == 0, out.stderr[-2000:]
+    r = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][0])
+    on, off = r["overlap_trial_ms"]
+    assert r["overlap_mode"] == "auto" and on > 0 and off > 0
+    assert r["overlap"] == (on <= off)
