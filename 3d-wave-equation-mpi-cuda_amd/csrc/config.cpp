@@ -40,7 +40,7 @@ std::string usage() {
            "  --rccl-mirror          with --ranks P: also send every halo message (and the error\n"
            "                         allreduce) through a 1-rank RCCL communicator, compare bitwise\n"
            "  --no-halo-check        skip the init-time halo self-test (patterns through the real plan)\n"
-           "  --device d  --threads t  --print-layers  --quiet\n";
+           "  --device d  --threads t  --no-print-layers  --quiet\n";
 }
 
 namespace {
@@ -203,6 +203,8 @@ Config parse_cli(const std::vector<std::string>& a) {
             c.threads = parse_int(need(i++), "threads");
         } else if (o == "--print-layers") {
             c.print_layers = true;
+        } else if (o == "--no-print-layers") {
+            c.print_layers = false;
         } else if (o == "--quiet") {
             c.quiet = true;
         } else {

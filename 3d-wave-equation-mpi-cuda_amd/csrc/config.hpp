@@ -64,7 +64,9 @@ struct Config {
     std::string fault;              // fault injection spec, e.g. "drop_face:1:5" (or env WAVE_FI)
     int device = -1;                // explicit device id (default: local rank)
     int threads = 0;                // CPU backend OpenMP threads (0 = Np)
-    bool print_layers = false;      // "calculating layer n" lines (reference stdout)
+    bool print_layers = true;       // "calculating layer n" lines on stdout (rank 0), as the
+                                    // reference (cuda_sol.cpp:385, hybrid_new.cpp:340); off with
+                                    // --no-print-layers or --quiet
     std::string dump;               // write the final layer as .npy (print_layer analogue)
 };
 

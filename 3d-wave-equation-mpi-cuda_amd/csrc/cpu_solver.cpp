@@ -411,7 +411,7 @@ private:
         res.aborted = false;
         int done = start - 1;
         for (int n = start; n <= K; ++n) {
-            if (cfg_.print_layers && local_ranks_[0] == 0) std::cout << "calculating layer " << n << "\n";
+            if (cfg_.print_layers && !cfg_.quiet && local_ranks_[0] == 0) std::cout << "calculating layer " << n << "\n";
             auto tl = clk::now();
             for (auto& R : ranks_) {
                 zero_faces(R, n);

@@ -172,7 +172,10 @@ public:
         const bool halos = msgs || fault_.kind == "drop_face";
         fine_ = cfg_.profile || halos;
         // every mark of a solve: IC + per sweep (compute, exchange) + reduction
-        ts_cap_ = size_t(6) * (prob_.K + 4) + 16;
+        ts_cap_ = size_t(12) * (prob_.K + 4) + 16;
+        ev_marks_.resize(ts_cap_, nullptr);
+        for (auto& e : ev_marks_) HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDefault));
+        no_timers_ = std::getenv("WAVE3D_NO_TIMERS") && std::string(std::getenv("WAVE3D_NO_TIMERS")) == "1";
         void* h = nullptr;
         HIP_CHECK(hipHostMalloc(&h, ts_cap_ * sizeof(u64), hipHostMallocCoherent | hipHostMallocMapped));
         ts_host_ = static_cast<u64*>(h);
@@ -460,6 +463,9 @@ private:
         if (s_comm_) (void)hipStreamDestroy(s_comm_);
         for (auto e : {ev_start_, ev_end_, ev_layer_, ev_halo_, ev_shell_})
             if (e) (void)hipEventDestroy(e);
+        for (auto e : ev_marks_)
+            if (e) (void)hipEventDestroy(e);
+        ev_marks_.clear();
         if (ts_host_) (void)hipHostFree(ts_host_);
         ts_host_ = ts_dev_ = nullptr;
         if (gexec_) (void)hipGraphExecDestroy(gexec_);
@@ -679,8 +685,13 @@ private:
                 snd.push_back({m.peer, m.tag, tb_ptr(R, m, mD), size_t(m.nplanes) * R.gv.si * sizeof(T)});
             for (auto& m : R.tb_recvs)
                 rcv.push_back({m.peer, m.tag, tb_ptr(R, m, mD), size_t(m.nplanes) * R.gv.si * sizeof(T)});
-            if (!snd.empty() || !rcv.empty()) ext_->exchange(snd, rcv, s);
+            if (!snd.empty() || !rcv.empty()) {
+                mark(s, 6);
+                ext_->exchange(snd, rcv, s);
+                mark(s, 7);
+            }
         } else {
+            mark(s, 6);
             for (auto& S : ranks_)
                 for (auto& m : S.tb_sends) {
                     auto& D = ranks_[m.peer];
@@ -695,6 +706,7 @@ private:
                         }
                     W3D_REQUIRE(done, "unmatched tb halo message");
                 }
+            mark(s, 7);
         }
         // y then z rounds: pack -> transport / D2D -> unpack, strictly after the x planes
         for (int rd = 0; rd < 2; ++rd) {
@@ -727,8 +739,11 @@ private:
                 std::vector<Message> snd, rcv;
                 for (auto& m : R.tb_bsends[rd]) snd.push_back({m.peer, m.tag, m.buf, bytes(m)});
                 for (auto& m : R.tb_brecvs[rd]) rcv.push_back({m.peer, m.tag, m.buf, bytes(m)});
+                mark(s, 6);
                 ext_->exchange(snd, rcv, s);
+                mark(s, 7);
             } else {
+                mark(s, 6);
                 for (auto& S : ranks_)
                     for (auto& m : S.tb_bsends[rd]) {
                         bool done = false;
@@ -741,6 +756,7 @@ private:
                             }
                         W3D_REQUIRE(done, "unmatched tb box halo message");
                     }
+                mark(s, 7);
             }
             for (auto& R : ranks_) {
                 auto o = ops(R, R.tb_brecvs[rd]);
@@ -873,11 +889,16 @@ private:
             for (size_t m = 0; m < R.plan.recvs.size(); ++m)
                 rcv.push_back({R.plan.recvs[m].peer, R.plan.recvs[m].tag, recv_ptr(R, m, n),
                                size_t(R.plan.recvs[m].count) * sizeof(T)});
-            if (!snd.empty() || !rcv.empty()) ext_->exchange(snd, rcv, s);
+            if (!snd.empty() || !rcv.empty()) {
+                mark(s, 6);
+                ext_->exchange(snd, rcv, s);
+                mark(s, 7);
+            }
             pack_faces(R, n, s, false);
             inject_after_exchange(R, n, s);
             return;
         }
+        mark(s, 6);
         for (auto& S : ranks_)
             for (size_t m = 0; m < S.plan.sends.size(); ++m) {
                 const auto& f = S.plan.sends[m];
@@ -895,6 +916,7 @@ private:
                 }
                 W3D_REQUIRE(done, "unmatched halo message");
             }
+        mark(s, 7);
         for (auto& R : ranks_) {
             pack_faces(R, n, s, false);
             inject_after_exchange(R, n, s);
@@ -1139,27 +1161,35 @@ private:
         log_msg(LogLevel::Info, "halo self-test: ", nreg, " messages verified");
     }
 
-    // Phase timers (the reference's C26 breakdown, mpi_new.cpp:33-34,368-371, in every run):
-    // a one-lane kernel stamps the device wall clock into a pinned host array at each mark,
-    // in stream order — captured into the hipGraph like any kernel (graph-captured event
-    // records carry no timestamps on this HIP). Slots: 0/1 compute (loop), 2/3 halo exchange
-    // (comm stream when overlapped), 4/5 final error reduction. Per-sweep ("fine") marks
-    // whenever halos move; a run without any exchange gets one loop interval around the
-    // IC + time loop instead (nothing between its kernels).
+    // Phase timers (the reference's C26 breakdown, mpi_new.cpp:33-34,368-371, in every run).
+    // Slots: 0/1 compute (loop), 2/3 halo exchange incl. pack/unpack (comm stream when
+    // overlapped), 4/5 final error reduction, 6/7 the transport itself (RCCL group / loopback
+    // copies: the reference's "MPI exchange" time; 2/3 minus 6/7 is its "host-device
+    // exchange"). Per-sweep ("fine") marks whenever halos move; a run without any exchange gets
+    // one loop interval around the IC + time loop instead (nothing between its kernels).
+    // Direct launches record timing events (a stream marker, no kernel); inside a hipGraph
+    // capture — where event records carry no timestamps on this HIP — a one-lane kernel stamps
+    // the device wall clock into pinned host memory instead. WAVE3D_NO_TIMERS=1 drops every
+    // fine mark (the A/B baseline of the timer cost).
     enum MarkMode { kAlways, kFine, kCoarse };
     void mark(hipStream_t s, int slot, MarkMode m = kFine) {
         if ((m == kFine && !fine_) || (m == kCoarse && fine_)) return;
+        if (no_timers_ && m != kAlways) return;
         if (tn_ >= ts_cap_) return;  // capacity is sized for every mark of a solve
-        launch_stamp(ts_dev_, int(tn_), s);
+        if (capturing_ || stamped_) launch_stamp(ts_dev_, int(tn_), s);
+        else HIP_CHECK(hipEventRecord(ev_marks_[tn_], s));
         if (tn_ < tslot_.size()) tslot_[tn_] = slot;
         else tslot_.push_back(slot);
         ++tn_;
     }
 
-    // device progress for the transport watchdog: marks of this solve stamped so far
+    // device progress for the transport watchdog: marks of this solve completed so far
     long progress() {
-        while (prog_seen_ < tn_ && reinterpret_cast<volatile u64*>(ts_host_)[prog_seen_] != 0)
-            ++prog_seen_;
+        if (stamped_) {
+            while (prog_seen_ < tn_ && reinterpret_cast<volatile u64*>(ts_host_)[prog_seen_] != 0) ++prog_seen_;
+        } else {
+            while (prog_seen_ < tn_ && hipEventQuery(ev_marks_[prog_seen_]) == hipSuccess) ++prog_seen_;
+        }
         return long(prog_seen_);
     }
 
@@ -1183,11 +1213,15 @@ private:
         if (gexec_) {
             // the whole IC + time loop as one graph launch (no per-kernel host overhead); its
             // timer marks were captured with it
+            if (cfg_.print_layers && !cfg_.quiet && ranks_[0].topo.rank == 0)
+                for (int q = 1; q <= K; ++q) std::cout << "calculating layer " << q << "\n";
             tn_ = graph_tn_;
+            stamped_ = true;
             HIP_CHECK(hipGraphLaunch(gexec_, s_comp_));
             res.layers_done = K;
         } else {
             tn_ = 0;
+            stamped_ = false;
             int start = 1;
             if (!cfg_.resume_dir.empty()) {
                 start = load_checkpoints() + 1;
@@ -1261,7 +1295,7 @@ private:
             const int span = (tbd_ == 3 && n + 2 <= K) ? 3 : ((tb_ && n + 1 <= K) ? 2 : 1);
             bool comm_follows = false;  // the comm stream already runs behind this layer's shells
             for (int q = n; q < n + span; ++q) guard_checkpoint_level(lvl(q), s_comp_);
-            if (cfg_.print_layers && !cfg_.quiet && ranks_[0].topo.rank == 0)
+            if (cfg_.print_layers && !cfg_.quiet && !capturing_ && ranks_[0].topo.rank == 0)
                 for (int q = n; q < n + span; ++q) std::cout << "calculating layer " << q << "\n";
             mark(s_comp_, 0);
             for (int q = n; q < n + span; ++q)
@@ -1355,7 +1389,7 @@ private:
     bool graph_eligible() const {
         return cfg_.graph != 0 && !ext_ && !mirror_ && cfg_.check_every == 0 && cfg_.checkpoint_every == 0 &&
                cfg_.resume_dir.empty() && fault_.kind.empty() &&
-               !cfg_.print_layers;
+               true;
     }
 
     void build_graph(RunResult& res) {
@@ -1363,15 +1397,18 @@ private:
         hipGraph_t g = nullptr;
         try {
             HIP_CHECK(hipStreamBeginCapture(s_comp_, hipStreamCaptureModeThreadLocal));
+            capturing_ = true;
             tn_ = 0;
             enqueue_ic();
             enqueue_layers(res, 1);
             graph_tn_ = tn_;
+            capturing_ = false;
             HIP_CHECK(hipStreamEndCapture(s_comp_, &g));
             HIP_CHECK(hipGraphInstantiate(&gexec_, g, nullptr, nullptr, 0));
             HIP_CHECK(hipGraphDestroy(g));
             log_msg(LogLevel::Info, "captured IC + ", prob_.K, " layers as one hipGraph");
         } catch (const Error& e) {
+            capturing_ = false;
             hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
             if (hipStreamIsCapturing(s_comp_, &st) == hipSuccess && st != hipStreamCaptureStatusNone) {
                 hipGraph_t h = nullptr;
@@ -1421,19 +1458,22 @@ private:
 
     void collect_profile(Timings& tm) {
         HIP_CHECK(hipDeviceSynchronize());
-        double sum[3] = {0, 0, 0};  // loop, exchange, error
+        double sum[4] = {0, 0, 0, 0};  // loop, exchange, error, transport
         for (size_t q = 0; q + 1 < tn_; ++q) {
             const int a = tslot_[q];
-            if (a != 0 && a != 2 && a != 4) continue;
+            if (a % 2) continue;
             for (size_t r = q + 1; r < tn_; ++r)
                 if (tslot_[r] == a + 1) {
-                    sum[a / 2] += double(i64(ts_host_[r] - ts_host_[q])) / clock_khz_;
+                    float ms = 0;
+                    if (stamped_) ms = float(double(i64(ts_host_[r] - ts_host_[q])) / clock_khz_);
+                    else HIP_CHECK(hipEventElapsedTime(&ms, ev_marks_[q], ev_marks_[r]));
+                    sum[a / 2] += ms;
                     break;
                 }
         }
         tm.loop_ms = sum[0];
         tm.exchange_ms = sum[1];
-        tm.comm_ms = sum[1];
+        tm.comm_ms = sum[3];
         tm.error_ms = sum[2];
     }
 
@@ -1670,6 +1710,10 @@ private:
     size_t graph_tn_ = 0;          // marks captured in the hipGraph
     size_t prog_seen_ = 0;         // marks known complete (watchdog progress)
     bool fine_ = false;            // per-sweep marks (halos move, or --profile)
+    bool capturing_ = false;       // inside the hipGraph capture: marks are stamp kernels
+    bool stamped_ = false;         // this solve's marks are stamps (graph replay), not events
+    bool no_timers_ = false;       // WAVE3D_NO_TIMERS=1: fine marks off (timer-cost A/B)
+    std::vector<hipEvent_t> ev_marks_;  // timing events of the direct-launch marks
     double init_ms_ = 0;
 };
 

@@ -223,7 +223,7 @@ def main() -> int:
         "courant": round(prob.courant, 4),
         "solver_ms_per_step": round(sum(res["solve_ms"]) / max(1, len(res["solve_ms"])), 4),
         # the reference's timer breakdown of the last solve, max over ranks (mpi_new.cpp:368-371)
-        "timers_ms": {k: round(res[k], 4) for k in ("loop_ms", "exchange_ms", "error_ms", "total_ms")},
+        "timers_ms": {k: round(res[k], 4) for k in ("loop_ms", "exchange_ms", "comm_ms", "error_ms", "total_ms")},
         "baseline_mpts": base,
     }
     if rank == 0:

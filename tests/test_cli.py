@@ -70,6 +70,27 @@ def test_cuda_format(cpu_prog, tmp_path):
     assert all(l.endswith(" ms") for l in lines[-4:])
 
 
+def test_cuda_format_four_distinct_timers(cpu_prog, tmp_path):
+    """cuda_sol's four totals (cuda_sol.cpp:438-441) are four different measurements: with
+    halos moving, host-device exchange = the pack/unpack around the transport (exchange minus
+    transport), MPI exchange = the transport itself, loop = stencil kernels."""
+    out = subprocess.run([cpu_prog, "48", "1", "pi", "pi", "pi", "1", "20", "--ranks", "4", "--format", "cuda",
+                          "--out-name", "c.txt", "--json", "--threads", "2"], cwd=tmp_path, capture_output=True,
+                         text=True, timeout=120, check=True)
+    import json
+
+    d = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][-1])
+    lines = open(tmp_path / "c.txt").read().splitlines()
+    vals = {l.split(":")[0]: float(l.split(":")[1].split()[0]) for l in lines[-4:]}
+    assert vals["total MPI exchange time"] == pytest.approx(d["comm_ms"], rel=1e-4, abs=1e-3)
+    assert vals["total host-device exchange time"] == pytest.approx(d["exchange_ms"] - d["comm_ms"], rel=1e-3,
+                                                                    abs=1e-3)
+    assert vals["total loop time"] == pytest.approx(d["loop_ms"], rel=1e-4, abs=1e-3)
+    assert d["exchange_ms"] > d["comm_ms"] > 0
+    # the reference's stdout: "calculating layer n" per layer by default (cuda_sol.cpp:385)
+    assert "calculating layer 20" in out.stdout
+
+
 def test_strict_cfl_refuses(cpu_prog, tmp_path):
     out = subprocess.run([cpu_prog, "512", "1", "pi", "pi", "pi", "1", "20", "--strict-cfl"],
                          cwd=tmp_path, capture_output=True, text=True, timeout=60)
