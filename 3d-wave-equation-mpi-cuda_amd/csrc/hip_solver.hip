@@ -16,6 +16,7 @@
 #include <chrono>
 #include <cstring>
 #include <iostream>
+#include <map>
 #include <memory>
 #include <thread>
 
@@ -939,13 +940,15 @@ private:
     }
 
     int mirror_slot(int src, int dst, int tag) {
-        const std::string key = "rank " + std::to_string(src) + " -> rank " + std::to_string(dst) + " tag " +
-                                std::to_string(tag);
-        for (size_t q = 0; q < mirror_keys_.size(); ++q)
-            if (mirror_keys_[q] == key) return int(q);
+        const i64 key = (i64(src) << 40) | (i64(dst) << 20) | i64(tag & 0xFFFFF);
+        auto it = mirror_index_.find(key);
+        if (it != mirror_index_.end()) return it->second;
         W3D_REQUIRE(mirror_keys_.size() < kMirrorSlots, "too many distinct halo messages for the rccl mirror");
-        mirror_keys_.push_back(key);
-        return int(mirror_keys_.size()) - 1;
+        mirror_keys_.push_back("rank " + std::to_string(src) + " -> rank " + std::to_string(dst) + " tag " +
+                               std::to_string(tag));
+        const int slot = int(mirror_keys_.size()) - 1;
+        mirror_index_[key] = slot;
+        return slot;
     }
 
     void setup_mirror() {
@@ -1677,12 +1680,13 @@ private:
     int trials_done_ = 0;         // overlap auto trials run (on, off)
     double trial_ms_[2] = {0, 0};
     bool xself_ = false;  // --x-self-transport
-    static constexpr size_t kMirrorSlots = 64;
+    static constexpr size_t kMirrorSlots = 2048;
     std::unique_ptr<RcclTransport> mirror_;  // --rccl-mirror: 1-rank communicator
     void* mirror_buf_ = nullptr;
     size_t mirror_bytes_ = 0;
     u64* mirror_res_ = nullptr;              // per message kind: differing words, first word
     std::vector<std::string> mirror_keys_;
+    std::map<i64, int> mirror_index_;
     long mirror_msgs_ = 0;                   // messages mirrored (all solves)
     bool selftest_ = false;  // inside halo_self_test()
     int halo_checked_ = 0;   // messages verified by the init-time halo self-test
