@@ -98,6 +98,7 @@ py::dict result_dict(const Config& c, const RunResult& r) {
     d["overlap_trial_ms"] = py::make_tuple(r.overlap_trial_ms[0], r.overlap_trial_ms[1]);
     d["comm_size"] = r.comm_size;
     d["halo_checked"] = r.halo_checked;
+    d["overlap_interior"] = r.overlap_interior;
     d["rccl_mirror_msgs"] = r.rccl_mirror_msgs;
     d["report"] = format_report(c, r);
     d["output_file"] = output_filename(c, r);
@@ -460,7 +461,8 @@ PYBIND11_MODULE(_wave3d_C, m) {
         for (int r = 0; r < n; ++r) out.append(py::make_tuple(t[r], errs[r]));
         return out;
     }, py::arg("n"), py::arg("fail_rank"), py::arg("fail_after_s"), py::arg("limit_s"));
-    m.def("checkpoint_layers", &checkpoint_layers, py::arg("dir"), py::arg("rank"),
+    m.def("checkpoint_layers", [](const std::string& dir, int rank) { return checkpoint_layers(dir, rank); },
+          py::arg("dir"), py::arg("rank"),
           "Layers with a complete checkpoint file of `rank` in `dir` (ascending).");
     m.def("encode_max_key", &encode_max_key);
     m.def("decode_max_key", &decode_max_key);

@@ -8,6 +8,7 @@
 #include <algorithm>
 #include <cerrno>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <fstream>
 #include <functional>
@@ -77,9 +78,19 @@ bool read_header(const std::string& path, CheckpointHeader& h) {
 
 }  // namespace
 
+void make_dirs(const std::string& dir) {  // mkdir -p
+    for (size_t p = 1; p <= dir.size(); ++p)
+        if (p == dir.size() || dir[p] == '/') {
+            const std::string sub = dir.substr(0, p);
+            if (::mkdir(sub.c_str(), 0755) != 0 && errno != EEXIST)
+                throw Error("cannot create checkpoint directory " + sub + ": " + std::strerror(errno));
+        }
+}
+
 void write_checkpoint(const std::string& dir, const CheckpointHeader& h, const HostLevel& prev,
                       const HostLevel& cur, const std::vector<double>& max_abs,
                       const std::vector<double>& max_rel) {
+    make_dirs(dir);
     const std::string path = checkpoint_path(dir, h.rank, h.layer);
     const std::string tmp = path + ".tmp";
     const int fd = ::open(tmp.c_str(), O_WRONLY | O_CREAT | O_TRUNC, 0644);
@@ -102,7 +113,17 @@ void write_checkpoint(const std::string& dir, const CheckpointHeader& h, const H
     fsync_dir(dir);
 }
 
-std::vector<int> checkpoint_layers(const std::string& dir, int rank) {
+bool same_run(const CheckpointHeader& h, const CheckpointHeader& e) {
+    bool same = std::memcmp(h.magic, e.magic, 8) == 0 && h.N == e.N && h.K == e.K && h.nprocs == e.nprocs &&
+                h.rank == e.rank && h.elem_size == e.elem_size && h.pi_mode == e.pi_mode &&
+                h.ic_mode == e.ic_mode && h.T == e.T && h.Lx == e.Lx && h.Ly == e.Ly && h.Lz == e.Lz &&
+                h.scheme == e.scheme;
+    for (int a = 0; a < 3; ++a)
+        same = same && h.dims[a] == e.dims[a] && h.coords[a] == e.coords[a] && h.ext[a] == e.ext[a];
+    return same;
+}
+
+std::vector<int> checkpoint_layers(const std::string& dir, int rank, const CheckpointHeader* match) {
     std::vector<int> out;
     DIR* d = ::opendir(dir.c_str());
     if (!d) return out;
@@ -112,35 +133,40 @@ std::vector<int> checkpoint_layers(const std::string& dir, int rank) {
         if (name.rfind(pre, 0) != 0 || name.size() < pre.size() + 5) continue;
         if (name.compare(name.size() - 4, 4, ".bin") != 0) continue;  // skips *.bin.tmp
         const std::string num = name.substr(pre.size(), name.size() - pre.size() - 4);
-        if (num.empty() || num.find_first_not_of("0123456789") != std::string::npos) continue;
+        // digits only, at most 9 of them (a layer is an int): anything else is not ours
+        if (num.empty() || num.size() > 9 || num.find_first_not_of("0123456789") != std::string::npos) continue;
         CheckpointHeader h;
-        const int layer = std::stoi(num);
-        if (read_header(dir + "/" + name, h) && h.layer == layer && h.rank == rank) out.push_back(layer);
+        const int layer = int(std::strtol(num.c_str(), nullptr, 10));
+        if (read_header(dir + "/" + name, h) && h.layer == layer && h.rank == rank && (!match || same_run(h, *match)))
+            out.push_back(layer);
     }
     ::closedir(d);
     std::sort(out.begin(), out.end());
     return out;
 }
 
-void prune_checkpoints(const std::string& dir, int rank, int keep) {
-    const std::vector<int> l = checkpoint_layers(dir, rank);
+void prune_checkpoints(const std::string& dir, const CheckpointHeader& mine, int newest, int keep) {
+    std::vector<int> l = checkpoint_layers(dir, mine.rank, &mine);
+    for (int n : l)
+        if (n > newest) (void)std::remove(checkpoint_path(dir, mine.rank, n).c_str());
+    l.erase(std::remove_if(l.begin(), l.end(), [&](int n) { return n > newest; }), l.end());
     for (size_t q = 0; q + size_t(keep) < l.size(); ++q)
-        (void)std::remove(checkpoint_path(dir, rank, l[q]).c_str());
+        (void)std::remove(checkpoint_path(dir, mine.rank, l[q]).c_str());
 }
 
-int agree_resume_layer(const std::string& dir, const std::vector<int>& local_ranks, Transport* ext) {
+int agree_resume_layer(const std::string& dir, const std::vector<CheckpointHeader>& expect, Transport* ext) {
     // newest layer complete on every local rank (ranks keep two generations, see header)
     double neg = -1e300;  // max over ranks of -(newest common layer) = -(min)
-    for (int r : local_ranks) {
-        const std::vector<int> l = checkpoint_layers(dir, r);
-        W3D_REQUIRE(!l.empty(), "no checkpoint of rank " + std::to_string(r) + " in " + dir);
+    for (const auto& e : expect) {
+        const std::vector<int> l = checkpoint_layers(dir, e.rank, &e);
+        W3D_REQUIRE(!l.empty(), "no checkpoint of rank " + std::to_string(e.rank) + " for this configuration in " + dir);
         neg = std::max(neg, -double(l.back()));
     }
     if (ext) ext->allreduce_max_host(&neg, 1);
     const int n = int(-neg);
     double missing = 0;
-    for (int r : local_ranks) {
-        const std::vector<int> l = checkpoint_layers(dir, r);
+    for (const auto& e : expect) {
+        const std::vector<int> l = checkpoint_layers(dir, e.rank, &e);
         if (!std::binary_search(l.begin(), l.end(), n)) missing = 1;
     }
     if (ext) ext->allreduce_max_host(&missing, 1);
@@ -158,15 +184,8 @@ int read_checkpoint(const std::string& dir, const CheckpointHeader& expect, cons
     CheckpointHeader h;
     f.read(reinterpret_cast<char*>(&h), sizeof(h));
     W3D_REQUIRE(f.good() && std::memcmp(h.magic, expect.magic, 8) == 0, "not a checkpoint: " + path);
-    bool same = h.N == expect.N && h.K == expect.K && h.nprocs == expect.nprocs &&
-                h.rank == expect.rank && h.elem_size == expect.elem_size &&
-                h.pi_mode == expect.pi_mode && h.ic_mode == expect.ic_mode && h.T == expect.T &&
-                h.Lx == expect.Lx && h.Ly == expect.Ly && h.Lz == expect.Lz && h.layer == expect.layer &&
-                h.scheme == expect.scheme;
-    for (int a = 0; a < 3; ++a)
-        same = same && h.dims[a] == expect.dims[a] && h.coords[a] == expect.coords[a] &&
-               h.ext[a] == expect.ext[a];
-    W3D_REQUIRE(same, "checkpoint " + path + " does not match this configuration");
+    W3D_REQUIRE(same_run(h, expect) && h.layer == expect.layer,
+                "checkpoint " + path + " does not match this configuration");
     const int n = h.layer;
     W3D_REQUIRE(n >= 1 && n < h.K, "checkpoint layer out of range");
     max_abs.assign(n + 1, 0.0);

@@ -38,13 +38,20 @@ struct CheckpointHeader {
 
 CheckpointHeader make_header(const Config& c, const Topology& t, int layer, int elem_size);
 std::string checkpoint_path(const std::string& dir, int rank, int layer);
-// Layers for which `rank` has a complete checkpoint file in `dir`, ascending.
-std::vector<int> checkpoint_layers(const std::string& dir, int rank);
-// Remove the rank's files older than its `keep` newest complete generations.
-void prune_checkpoints(const std::string& dir, int rank, int keep = 2);
+// Same run: every header field but the layer (N, K, decomposition, physics, dtype, scheme).
+bool same_run(const CheckpointHeader& a, const CheckpointHeader& b);
+// Layers for which `rank` has a complete checkpoint file in `dir`, ascending; with `match`,
+// only files written by the same run configuration (a directory may hold files of others).
+std::vector<int> checkpoint_layers(const std::string& dir, int rank, const CheckpointHeader* match = nullptr);
+// After this run wrote layer `newest`: remove the rank's files of this configuration with a
+// higher layer (left by an earlier run that got further: never newer state than this run's),
+// then every one older than the `keep` newest complete generations. Files of other
+// configurations are left alone.
+void prune_checkpoints(const std::string& dir, const CheckpointHeader& mine, int newest, int keep = 2);
 // The resume layer: newest layer for which every rank (the local ones, and every process
-// through `ext` when given) has a complete file; throws if some rank lacks it.
-int agree_resume_layer(const std::string& dir, const std::vector<int>& local_ranks, Transport* ext);
+// through `ext` when given) has a complete file matching its expected header (`expect`, one
+// per local rank, layer ignored); throws if some rank lacks it.
+int agree_resume_layer(const std::string& dir, const std::vector<CheckpointHeader>& expect, Transport* ext);
 
 // Host view of one level: element (i,j,k) of the owned block (1..X, 1..Y, 1..Z) lives at
 // origin + (i*si + j*sj + k) elements. Only owned nodes are stored.

@@ -474,7 +474,7 @@ private:
             // leapfrog keeps u^{n-1} (slot (n+2)%3), the increment form d^n (slot (n+1)%3)
             write_checkpoint(cfg_.checkpoint_dir, h, host_level(R, (n + (cfg_.delta ? 1 : 2)) % 3),
                              host_level(R, n % 3), a, r);
-            prune_checkpoints(cfg_.checkpoint_dir, R.topo.rank, 2);
+            prune_checkpoints(cfg_.checkpoint_dir, h, n, 2);
         }
     }
 
@@ -490,9 +490,9 @@ private:
     }
 
     int load_checkpoints() {
-        std::vector<int> lr;
-        for (auto& R : ranks_) lr.push_back(R.topo.rank);
-        const int n = agree_resume_layer(cfg_.resume_dir, lr, ext_);  // same layer on every rank
+        std::vector<CheckpointHeader> ex;
+        for (auto& R : ranks_) ex.push_back(make_header(cfg_, R.topo, 0, sizeof(T)));
+        const int n = agree_resume_layer(cfg_.resume_dir, ex, ext_);  // same layer on every rank
         for (auto& R : ranks_) {
             CheckpointHeader h = make_header(cfg_, R.topo, n, sizeof(T));
             read_checkpoint(cfg_.resume_dir, h, host_level(R, (n + (cfg_.delta ? 1 : 2)) % 3),

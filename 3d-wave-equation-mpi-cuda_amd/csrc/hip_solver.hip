@@ -143,8 +143,10 @@ public:
             // increment form: temporal blocking sweeps (u and d levels in the ring: after a
             // sweep, lvl(m+1) = u^{m+1}, lvl(m) = d^{m+1}); an odd last layer is one step of
             // the naive/flat kernel reading that d level
-            W3D_REQUIRE(tb_ && (tbd_ == 2 || tb3_delta_supported(tb_rows_, tb_waves_)),
-                        "--scheme delta needs a tb2 kernel or tb3 / tb3r1w8 (kernel auto, tb2*, tb3*)");
+            W3D_REQUIRE(tb_ && (tbd_ == 2 ? tb2_delta_supported(tb_rows_, tb_waves_, tb_nwk_) && tb_occ_ == 0
+                                          : tb3_delta_supported(tb_rows_, tb_waves_)),
+                        "--scheme delta needs a tb2 kernel with an increment-form instantiation (tb2, tb2r2w8, "
+                        "tb2r4w4, tb2r2w8k2) or tb3 / tb3r1w8");
             kind_ = KernelVariant{};
             kind_.march = false;
             kind_.delta = true;
@@ -230,6 +232,13 @@ public:
         res.scheme = cfg_.delta ? "delta" : "leapfrog";
         res.comm_size = ext_ ? ext_->comm_size() : 0;
         res.halo_checked = halo_checked_;
+        if (ext_ || world_ > 1) {
+            res.overlap_interior = -1;
+            for (auto& R : ranks_) {
+                const i64 c = (tb_ ? R.tb_interior : R.interior).count();
+                res.overlap_interior = res.overlap_interior < 0 ? c : std::min<long long>(res.overlap_interior, c);
+            }
+        }
         for (int a = 0; a < 3; ++a) res.dims[a] = ranks_[0].topo.dims[a];
         Timings t;
         solve(res, t);
@@ -1590,7 +1599,7 @@ private:
                 HIP_CHECK(hipEventSynchronize(ev));
                 for (size_t q = 0; q < hs.size(); ++q) {
                     write_checkpoint(dir, hs[q], lps[q], lcs[q], a, r);
-                    prune_checkpoints(dir, rk[q], 2);
+                    prune_checkpoints(dir, hs[q], n, 2);
                     log_msg(LogLevel::Info, "rank ", rk[q], ": checkpoint after layer ", n, " -> ",
                             checkpoint_path(dir, rk[q], n));
                 }
@@ -1625,9 +1634,9 @@ private:
 
     int load_checkpoints() {
         HIP_CHECK(hipDeviceSynchronize());
-        std::vector<int> lr;
-        for (auto& R : ranks_) lr.push_back(R.topo.rank);
-        const int n = agree_resume_layer(cfg_.resume_dir, lr, ext_);  // same layer on every rank
+        std::vector<CheckpointHeader> ex;
+        for (auto& R : ranks_) ex.push_back(make_header(cfg_, R.topo, 0, sizeof(T)));
+        const int n = agree_resume_layer(cfg_.resume_dir, ex, ext_);  // same layer on every rank
         for (auto& R : ranks_) {
             const int lp = lvl(n + L_ - 1), lc = lvl(n);
             std::vector<T> prev(R.elems, T(0)), cur(R.elems, T(0));

@@ -174,10 +174,10 @@ void RcclTransport::allreduce_max_host(double* data, size_t n) {
                                impl_->side));
     W3D_REQUIRE(impl_->comm, "RCCL communicator was aborted");
     settle(ncclAllReduce(impl_->scratch, impl_->scratch, n, ncclFloat64, ncclMax, impl_->comm, impl_->side),
-           watchdog_limit_s(), "RCCL allreduce");
+           host_collective_limit_s(), "RCCL allreduce");
     HIP_CHECK_T(hipMemcpyAsync(data, impl_->scratch, n * sizeof(double), hipMemcpyDeviceToHost,
                                impl_->side));
-    wait_stream(impl_->side);
+    wait_stream_limit(impl_->side, nullptr, host_collective_limit_s());
 }
 
 void RcclTransport::barrier() {
@@ -193,6 +193,22 @@ void RcclTransport::check_async() const {
 }
 
 bool RcclTransport::wait_stream(void* stream, const std::function<long()>* progress) {
+    wait_stream_limit(stream, progress, watchdog_limit_s());
+    return true;
+}
+
+// Host-level collectives (timers, the per-checkpoint error reduction, barriers) wait for the
+// slowest rank's host work — e.g. its checkpoint writer finishing an fsync of many GB — not for
+// device progress: they get the longer WAVE3D_HOST_WATCHDOG_S limit (default 1800 s).
+double host_collective_limit_s() {
+    static const double limit = [] {
+        const char* e = std::getenv("WAVE3D_HOST_WATCHDOG_S");
+        return e ? std::atof(e) : std::max(1800.0, watchdog_limit_s());
+    }();
+    return limit;
+}
+
+void RcclTransport::wait_stream_limit(void* stream, const std::function<long()>* progress, double limit_s) {
     hipStream_t s = static_cast<hipStream_t>(stream);
     watch_until(
         [&] {
@@ -206,13 +222,12 @@ bool RcclTransport::wait_stream(void* stream, const std::function<long()>* progr
             NCCL_CHECK(ncclCommGetAsyncError(impl_->comm, &st));
             return st == ncclSuccess || st == ncclInProgress ? std::string() : std::string(ncclGetErrorString(st));
         },
-        progress, watchdog_limit_s(),
+        progress, limit_s,
         [&] {
             if (impl_->comm) (void)ncclCommAbort(impl_->comm);
             impl_->comm = nullptr;
         },
         "RCCL");
-    return true;
 }
 
 // ---- TCP rendezvous -------------------------------------------------------------------

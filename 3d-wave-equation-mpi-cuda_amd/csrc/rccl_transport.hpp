@@ -21,6 +21,8 @@ std::string rccl_unique_id();  // 128 raw bytes
 // (<= 0: RCCL's own default)
 constexpr int kRcclDefaultMaxCtas = 8;
 int rccl_max_ctas();
+// Watchdog limit of host-level collectives (WAVE3D_HOST_WATCHDOG_S, default 1800 s)
+double host_collective_limit_s();
 
 class RcclTransport : public Transport {
 public:
@@ -49,6 +51,7 @@ public:
 
 private:
     void settle(int nccl_result, double limit_s, const char* what);
+    void wait_stream_limit(void* stream, const std::function<long()>* progress, double limit_s);
     struct Impl;
     std::unique_ptr<Impl> impl_;
     int rank_, size_;

@@ -42,6 +42,8 @@ struct RunResult {
     double overlap_trial_ms[2] = {0, 0};  // --overlap auto: solve time with overlap on / off
     int comm_size = 0;     // ranks the transport's communicator reports (ncclCommCount), 0 = none
     long rccl_mirror_msgs = 0;  // --rccl-mirror: messages sent through RCCL and compared
+    long long overlap_interior = -1;  // min over ranks of nodes in the interior box that runs
+                                      // concurrently with the halo (tb2/tb3: per sweep; -1: none)
     int halo_checked = 0;  // halo messages verified by the init-time self-test (0 = none ran)
 
     double points() const { return double(N + 1) * double(N + 1) * double(N + 1); }

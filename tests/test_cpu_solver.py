@@ -156,6 +156,40 @@ def test_checkpoint_generations_and_agreed_resume(C, tmp_path):
         _solve(p, ranks=3, resume=d)
 
 
+def test_checkpoint_stale_files_of_other_runs(C, tmp_path):
+    """A directory still holding higher-layer files of other runs (a longer K, another N, and
+    the same configuration run further before) neither makes pruning delete this run's
+    checkpoints nor makes resume pick a stale file (files are matched on the header)."""
+    import shutil
+
+    import wave3d
+
+    d = str(tmp_path)
+    other = tmp_path / "other"
+    # a longer run (K=30) and another N leave layers 24/27 and 12 behind for ranks 0..2
+    _solve(wave3d.WaveProblem(20, timesteps=30, ic="shifted"), ranks=3, checkpoint_every=3, checkpoint_dir=str(other))
+    _solve(wave3d.WaveProblem(22, timesteps=14, ic="shifted"), ranks=3, checkpoint_every=12,
+           checkpoint_dir=str(other / "n22"))
+    for f in os.listdir(other):
+        if f.endswith(".bin"):
+            shutil.copy(other / f, tmp_path / f)
+    for f in os.listdir(other / "n22"):
+        shutil.copy(other / "n22" / f, tmp_path / ("x" + f))  # different names must not matter
+    # the same configuration once left layer 13 behind; this run checkpoints layers 6 and 12:
+    # writing 6 removes the superseded 13 (it would otherwise outrank this run's files)
+    p = wave3d.WaveProblem(20, timesteps=14, ic="shifted")
+    _solve(p, ranks=3, checkpoint_every=13, checkpoint_dir=d)
+    for r in range(3):
+        assert C.checkpoint_layers(d, r) == [13, 24, 27]
+    full = _solve(p, ranks=3)
+    _solve(p, ranks=3, checkpoint_every=6, checkpoint_dir=d)
+    for r in range(3):
+        assert C.checkpoint_layers(d, r) == [6, 12, 24, 27]  # K=30's two newest survive untouched
+    res = _solve(p, ranks=3, resume=d)
+    assert res.extra["resumed_from"] == 12
+    assert res.max_abs == full.max_abs and res.max_rel == full.max_rel
+
+
 def test_checkpoint_agreed_resume_multiprocess(C, tmp_path):
     """The same agreement across processes (gloo host transport, 2 ranks): rank 1's newest
     checkpoint is missing, both processes resume from layer 9 and reproduce the full run."""
