@@ -54,6 +54,13 @@ def main() -> int:
     ap.add_argument("--fill-hbm", type=float, default=0.0,
                     help="size N to this fraction of each GPU's HBM (SURVEY §7.3; e.g. 0.9)")
     ap.add_argument("--dtype", default="fp64", choices=["fp64", "fp32"])
+    ap.add_argument("--scheme", default="auto", choices=["auto", "leapfrog", "delta"],
+                    help="time stepping: leapfrog (the reference's), delta (increment form, same scheme "
+                         "without the 2u-u cancellation); auto = leapfrog for fp64, delta for fp32 "
+                         "(profiles/fp32_scheme_r3.txt)")
+    ap.add_argument("--fp64-ref", default="auto", choices=["auto", "on", "off"],
+                    help="fp32 runs: after timing, solve the same N/K/decomposition in fp64 and report "
+                         "its L-inf as linf_fp64_ref (BASELINE.md §4 config 5); auto = on for fp32")
     ap.add_argument("--kernel", default="auto")
     ap.add_argument("--chunk", type=int, default=0)
     ap.add_argument("--overlap", default="auto", choices=["auto", "on", "off"],
@@ -125,6 +132,8 @@ def main() -> int:
                   file=sys.stderr)
         np_ = named["problem"]
         a.N, a.timesteps, a.dtype = np_.N, np_.timesteps, np_.dtype
+        if a.scheme == "auto":
+            a.scheme = np_.scheme
         if named["dims"] and not a.dims and named["Np"] == n_gpus:
             a.dims = ",".join(str(x) for x in named["dims"])
         plan = dict(plan, config=a.config, golden=presets.GOLDEN_LINF.get((np_.N, np_.timesteps)))
@@ -143,7 +152,9 @@ def main() -> int:
         K = wave3d.WaveProblem(N, dtype=a.dtype).min_stable_timesteps()
         K = max(20, int(K * 0.577 / 0.5) + 1)  # C <= 0.5
     a.timesteps = K
-    prob = wave3d.WaveProblem(N, timesteps=a.timesteps, dtype=a.dtype)
+    if a.scheme == "auto":
+        a.scheme = presets.default_scheme(a.dtype)
+    prob = wave3d.WaveProblem(N, timesteps=a.timesteps, dtype=a.dtype, scheme=a.scheme)
     if not prob.stable():
         print(f"bench: warning: C={prob.courant:.3f} > 1/sqrt(3) (unstable)", file=sys.stderr)
     solver = wave3d.WaveSolver(prob, a.backend, transport=transport, Np=n_gpus, kernel=a.kernel, dims=dims,
@@ -190,9 +201,10 @@ def main() -> int:
         "scaling": "strong" if a.N else plan["scaling"],  # --N fixes the global grid
         "vs_baseline": round(value / base, 3),
         "dtype": a.dtype,
+        "scheme": res.get("scheme", a.scheme),
         "data": "synthetic (analytic initial condition u=sin(2pi x/Lx)sin(pi y/Ly)sin(pi z/Lz))",
         "config": {
-            "model": f"wave3d leapfrog 7-point, N={N}^3, L=pi, T=1, timesteps={a.timesteps}",
+            "model": f"wave3d {a.scheme} 7-point, N={N}^3, L=pi, T=1, timesteps={a.timesteps}",
             "global_batch": 1,
             "seq_len": N + 1,
             "parallelism": f"dd{dims[0]}x{dims[1]}x{dims[2]}-{res['kernel']}"
@@ -226,13 +238,27 @@ def main() -> int:
         "timers_ms": {k: round(res[k], 4) for k in ("loop_ms", "exchange_ms", "comm_ms", "error_ms", "total_ms")},
         "baseline_mpts": base,
     }
-    if rank == 0:
-        print(json.dumps(out), flush=True)
     # explicit teardown while HIP and the process group are alive: the session (which keeps the
     # transport alive) first, then the transport (ncclCommDestroy), then the torch group
     del sess
-    transport = None
     import gc
+    gc.collect()
+    if a.dtype == "fp32" and a.fp64_ref != "off" or a.fp64_ref == "on":
+        # the fp64 L-inf of the same N, K and decomposition (config 5 compares
+        # against its own fp64 run), after the timed region and after the fp32 session is freed
+        p64 = wave3d.WaveProblem(N, timesteps=a.timesteps, dtype="fp64")
+        s64 = wave3d.WaveSolver(p64, a.backend, transport=transport, Np=n_gpus, kernel="auto", dims=dims,
+                                overlap="off" if a.no_overlap else a.overlap,
+                                device=(torch.cuda.current_device() if a.backend == "hip" else None))
+        r64 = s64.run()
+        out["linf_fp64_ref"] = r64.linf_abs
+        out["linf_fp64_ref_kernel"] = r64.kernel
+        out["linf_vs_fp64"] = round(out["linf_abs"] / r64.linf_abs, 3) if r64.linf_abs > 0 else None
+        del s64
+        gc.collect()
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    transport = None
     gc.collect()
     if world > 1:
         dist.barrier()

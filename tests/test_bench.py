@@ -106,15 +106,19 @@ def test_bench_gpu_multirank_plan_staged(n, N, dims):
 
 
 @pytest.mark.gpu
-def test_bench_gpu_fp32_two_ranks_staged():
+@pytest.mark.parametrize("scheme,linf", [("leapfrog", "4.47035e-06"), ("auto", "1.3113e-06")])
+def test_bench_gpu_fp32_two_ranks_staged(scheme, linf):
     """fp32 runs the three-layer sweep (tb3, 3-deep halos) through the multi-process bench path:
-    2 processes on one MI355X, staged transport, N=512 on 2x1x1 slabs, K=100 (stable): the
-    fp32 L-inf of the single-GPU run (4.47035e-06, profiles/fp32_accuracy_r2.txt)."""
+    2 processes on one MI355X, staged transport, N=512 on 2x1x1 slabs, K=100 (stable): the fp32
+    L-inf of the single-GPU run (leapfrog 4.47035e-06, profiles/fp32_accuracy_r2.txt; the fp32
+    default, the increment form, 1.3113e-06), and the fp64 L-inf of the same run (the golden)."""
     r = _bench(["--steps", "1", "--warmup", "0", "--dtype", "fp32", "--transport", "staged",
-                "--shared-device"], nproc=2, timeout=600)
+                "--shared-device", "--overlap", "on", "--scheme", scheme], nproc=2, timeout=600)
     assert r["dtype"] == "fp32" and r["n_gpus"] == 2 and r["config"]["dims"] == [2, 1, 1]
     assert r["config"]["kernel"] == "tb3" and r["config"]["overlap"] is True
-    assert f"{r['linf_abs']:.6g}" == "4.47035e-06"
+    assert r["scheme"] == ("delta" if scheme == "auto" else scheme)
+    assert f"{r['linf_abs']:.6g}" == linf
+    assert f"{r['linf_fp64_ref']:.6g}" == "6.03381e-07"
 
 
 def test_bench_named_config_cpu128():
