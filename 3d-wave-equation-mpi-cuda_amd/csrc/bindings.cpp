@@ -73,6 +73,7 @@ py::dict result_dict(const Config& c, const RunResult& r) {
     d["backend"] = r.backend;
     d["kernel"] = r.kernel;
     d["scheme"] = r.scheme;
+    d["math"] = r.math;
     d["transport"] = r.transport;
     d["courant"] = r.courant;
     d["max_abs"] = r.max_abs;
@@ -228,7 +229,7 @@ void k_tb2_dense(int rows, int waves, int nwk, bool delta, bool first, uintptr_t
 
 // One three-layer sweep (k_tb3): C = u^m (errors only), D = u^{m+1}, E = u^{m+2}.
 template <class T>
-void k_tb3_dense(int rows, int waves, bool first, uintptr_t A, uintptr_t B, uintptr_t D, uintptr_t E,
+void k_tb3_dense(int rows, int waves, bool fm, bool first, uintptr_t A, uintptr_t B, uintptr_t D, uintptr_t E,
                  const std::vector<i64>& g, const std::vector<std::vector<int>>& boxes,
                  const std::vector<int>& cdom, int ei0, int ei1, uintptr_t tx, uintptr_t ty,
                  uintptr_t tz, const std::vector<double>& cC, const std::vector<double>& cD,
@@ -244,7 +245,7 @@ void k_tb3_dense(int rows, int waves, bool first, uintptr_t A, uintptr_t B, uint
     if (hipMalloc(&txy, txy_elems(v.X, v.Y) * sizeof(T)) != hipSuccess) throw Error("k_tb3: hipMalloc failed");
     try {
         launch_txy<T>(txy, P<T>(tx), P<T>(ty), v.X, v.Y, s);
-        launch_tb3<T>(rows, waves, false, first, P<T>(A) + o, P<T>(B) + o, P<T>(D) + o, P<T>(E) + o, v,
+        launch_tb3<T>(rows, waves, false, fm, first, P<T>(A) + o, P<T>(B) + o, P<T>(D) + o, P<T>(E) + o, v,
                       bx.data(), int(bx.size()), tobox(cdom), ei0, ei1, Wrap{}, Wrap{},
                       SeamPartners<T>{}, txy, P<T>(tz), tocoefs(cC), tocoefs(cD),
                       tocoefs(cE), P<u64>(errC), P<u64>(errD), P<u64>(errE), chunk, s);
@@ -475,9 +476,9 @@ PYBIND11_MODULE(_wave3d_C, m) {
     m.def("k_tb2_f32", &k_tb2_dense<float>);
     m.def("k_tb3_f64", &k_tb3_dense<double>);
     m.def("k_tb3_f32", &k_tb3_dense<float>);
-    m.def("tb_supported", [](int depth, int rows, int waves, int nwk) {
-        return depth == 3 ? tb3_supported(rows, waves) : tb2_supported(rows, waves, 0, nwk);
-    }, py::arg("depth"), py::arg("rows"), py::arg("waves"), py::arg("nwk") = 1);
+    m.def("tb_supported", [](int depth, int rows, int waves, int nwk, bool fm) {
+        return depth == 3 ? tb3_supported(rows, waves, fm) : tb2_supported(rows, waves, 0, nwk);
+    }, py::arg("depth"), py::arg("rows"), py::arg("waves"), py::arg("nwk") = 1, py::arg("fm") = false);
     m.def("k_init_f64", &k_init<double>);
     m.def("k_init_f32", &k_init<float>);
     m.def("k_faces_f64", &k_faces<double>);

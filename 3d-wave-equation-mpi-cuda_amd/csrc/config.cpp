@@ -10,6 +10,8 @@ std::string usage() {
            "  Lx|Ly|Lz: number or the literal 'pi'\n"
            "options:\n"
            "  --dtype fp64|fp32      compute precision (default fp64)\n"
+           "  --math exact|fma       exact = the reference's operation order, bit for bit (default);\n"
+           "                         fma = coef/h^2 folded into fused multiply-adds (tb3 kernels)\n"
            "  --pi ref|exact         ref = 3.1415926535 as the reference CPU programs (default)\n"
            "  --scheme leapfrog|delta  delta = increment form (fp32 accuracy; tb2 kernels, CPU)\n"
            "  --ic ref|shifted       shifted = sin(2*pi*x/Lx + 0.7) periodic-BC check\n"
@@ -21,7 +23,7 @@ std::string usage() {
            "  --overlap auto|on|off  interior/shell split with the halo on a second stream; auto\n"
            "                         (default) times the first two solves on / off, keeps the faster\n"
            "  --no-overlap           = --overlap off\n"
-           "  --kernel K             auto (= tb2) | tb2[r<R>][w<W>] | tb3[r<R>w<W>] | march[2|4|8][nt|p|f]\n"
+           "  --kernel K             auto (fp64: tb2r2w8, fp32: tb3) | tb2[r<R>][w<W>] | tb3[r<R>w<W>] | march[2|4|8][nt|p|f]\n"
            "                         | naive | flat   (temporal blocking / single-step variants)\n"
            "  --chunk C              i-planes per marching work item\n"
            "  --format new|omp|cuda|none      output file flavour (default new)\n"
@@ -113,6 +115,11 @@ Config parse_cli(const std::vector<std::string>& a) {
             if (v == "leapfrog") c.delta = false;
             else if (v == "delta") c.delta = true;
             else throw Error("wave3d: bad --scheme " + v);
+        } else if (o == "--math") {
+            const std::string& v = need(i++);
+            if (v == "exact") c.fma = false;
+            else if (v == "fma") c.fma = true;
+            else throw Error("wave3d: bad --math " + v);
         } else if (o == "--pi") {
             const std::string& v = need(i++);
             if (v == "ref") c.pi = PiMode::Ref;

@@ -30,6 +30,8 @@ struct Config {
     bool delta = false;             // --scheme delta: increment form u^n = u^{n-1} + d^n,
                                     // d^n = d^{n-1} + a2 tau^2 lap u^{n-1} (same scheme in exact
                                     // arithmetic; no 2u - u cancellation, fp32 accuracy)
+    bool fma = false;               // --math fma: stencil update with coef/h^2 folded into FMAs
+                                    // (temporal-blocking kernels; not bitwise with the reference)
     PiMode pi = PiMode::Ref;
     ICMode ic = ICMode::Ref;
     int dims[3] = {0, 0, 0};        // 0 = let dims_create choose (MPI_Dims_create semantics)

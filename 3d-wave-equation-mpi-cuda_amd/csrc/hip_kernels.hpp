@@ -117,13 +117,14 @@ struct SeamCPlane {
     T* out = nullptr;
     const T *Ac = nullptr, *Am = nullptr, *Ap = nullptr, *Bc = nullptr;
 };
+// fm: --math fma instantiations (stencil_math coef_lap_fma), not bitwise with the reference
 template <class T>
-void launch_seam_c(bool first, bool delta, const SeamCPlane<T>* ops, int nops, const GridView& gv,
+void launch_seam_c(bool first, bool delta, bool fm, const SeamCPlane<T>* ops, int nops, const GridView& gv,
                    const Box& cdom, const StepCoefs& cC, hipStream_t s);
-bool tb3_supported(int rows, int waves);
-bool tb3_delta_supported(int rows, int waves);
+bool tb3_supported(int rows, int waves, bool fm = false);
+bool tb3_delta_supported(int rows, int waves, bool fm = false);
 template <class T>
-void launch_tb3(int rows, int waves, bool delta, bool first, const T* A, const T* B, T* D, T* E,
+void launch_tb3(int rows, int waves, bool delta, bool fm, bool first, const T* A, const T* B, T* D, T* E,
                 const GridView& gv, const Box* boxes, int nbox, const Box& cdom, int ei0, int ei1,
                 const Wrap& wrapD, const Wrap& wrapE, const SeamPartners<T>& seam, const T* txy,
                 const T* tz, const StepCoefs& cC, const StepCoefs& cD,

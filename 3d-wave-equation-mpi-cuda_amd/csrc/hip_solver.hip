@@ -133,6 +133,9 @@ public:
         G_ = lay.G;
         L_ = lay.L;
         for (int a = 0; a < 3; ++a) cfg_.dims[a] = lay.dims[a];
+        W3D_REQUIRE(!c.fma || (tb_ && tbd_ == 3 && (c.delta ? tb3_delta_supported(tb_rows_, tb_waves_, true)
+                                                              : tb3_supported(tb_rows_, tb_waves_, true))),
+                    "--math fma needs a three-layer kernel with an fma instantiation (tb3, tb3r1w8, tb3r1w16)");
         W3D_REQUIRE(!tb_ || (tbd_ == 3 ? tb3_supported(tb_rows_, tb_waves_)
                                         : tb2_supported(tb_rows_, tb_waves_, tb_occ_, tb_nwk_)),
                     "wave3d: unknown kernel variant " + c.kernel);
@@ -230,6 +233,7 @@ public:
                            : overlap_auto_       ? "auto"
                            : (overlap_ ? "on" : "off");
         res.scheme = cfg_.delta ? "delta" : "leapfrog";
+        res.math = cfg_.fma ? "fma" : "exact";
         res.comm_size = ext_ ? ext_->comm_size() : 0;
         res.halo_checked = halo_checked_;
         if (ext_ || world_ > 1) {
@@ -840,7 +844,7 @@ private:
     void seam_c(DevRank<T>& R, int m, hipStream_t s) {
         std::vector<SeamCPlane<T>> ops;
         seam_partners(R, m, &ops);
-        launch_seam_c<T>(m == 1, cfg_.delta, ops.data(), int(ops.size()), R.gv, R.cdom, coefs(m), s);
+        launch_seam_c<T>(m == 1, cfg_.delta, cfg_.fma, ops.data(), int(ops.size()), R.gv, R.cdom, coefs(m), s);
     }
 
     void sweep3(DevRank<T>& R, int m, hipStream_t s, const Box* boxes = nullptr, int nbox = 0) {
@@ -848,7 +852,7 @@ private:
         const T* B = R.g[lvl(m + L_ - 2)];
         const SeamPartners<T> sp = seam_partners(R, m, nullptr);
         if (!boxes) boxes = &R.compute, nbox = 1;
-        launch_tb3<T>(tb_rows_, tb_waves_, cfg_.delta, m == 1, A, B, R.g[lvl(m + 1)], R.g[lvl(m + 2)], R.gv, boxes,
+        launch_tb3<T>(tb_rows_, tb_waves_, cfg_.delta, cfg_.fma, m == 1, A, B, R.g[lvl(m + 1)], R.g[lvl(m + 2)], R.gv, boxes,
                       nbox, R.cdom, R.error.i0, R.error.i1, R.wrap2, R.wrap3, sp, R.txy, R.tz,
                       coefs(m), coefs(m + 1), coefs(m + 2), R.err + size_t(m) * kSlotsPerLayer,
                       R.err + size_t(m + 1) * kSlotsPerLayer, R.err + size_t(m + 2) * kSlotsPerLayer,

@@ -63,6 +63,7 @@ struct Tb3Params {
     const T* tz;
     T hx2, hy2, hz2, yx2, yy2, yz2;
     T coefC, coefD, coefE, ctC, ctD, ctE;
+    T fc[3][3];  // --math fma: coef/h^2 per layer (C, D, E) and axis
     u64* errC;
     u64* errD;
     u64* errE;
@@ -78,7 +79,9 @@ struct Tb3Params {
 // DELTA: increment form (as k_tb2): B = d^{m-1}; d^m = B + coefC lap A, C = A + d^m;
 // d^{m+1} = d^m + coefD lap C, D = C + d^{m+1}; d^{m+2} = d^{m+1} + coefE lap D, E = D + d^{m+2}.
 // The D level receives d^{m+2} (the next sweep's B), so the bytes moved are unchanged.
-template <class T, bool FIRST, int R, int NW, bool DELTA = false,
+// FM: --math fma (stencil_math coef_lap_fma): the update with coef/h^2 folded, not bitwise with
+// the reference CPU programs; fewer VALU operations per node (the fp64 sweep is issue-bound).
+template <class T, bool FIRST, int R, int NW, bool DELTA = false, bool FM = false,
           int WPE = (R == 1 || (DELTA && sizeof(T) == 4) ? 4 : 1)>
 __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WPE, 8))) k_tb3(const Tb3Params<T> p) {
     constexpr int TJ = NW * R;
@@ -234,12 +237,33 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WP
     RelArg<T> mr3;
     T chk1 = T(0), chk2 = T(0), chk3 = T(0);
 
-    auto lapA = [&](int H, int y, int x, T ctr, T xm, T xp) {
-        return laplace7_cr(ctr, xm, xp, ldsA[H][y - 1][x], ldsA[H][y + 1][x], ldsA[H][y][x - 1],
-                           ldsA[H][y][x + 1], p.hx2, p.hy2, p.hz2, p.yx2, p.yy2, p.yz2);
+    // Layer L (0 = C, 1 = D, 2 = E) arithmetic. lap(): the Laplacian (exact) or coef*Laplacian
+    // (FM); leap / first / incr: the leapfrog, Taylor-start and increment updates from it.
+    auto lap = [&](int L, T ctr, T xm, T xp, T ym, T yp, T zm, T zp) {
+        if constexpr (FM)
+            return coef_lap_fma(ctr, xm, xp, ym, yp, zm, zp, p.fc[L][0], p.fc[L][1], p.fc[L][2]);
+        else
+            return laplace7_cr(ctr, xm, xp, ym, yp, zm, zp, p.hx2, p.hy2, p.hz2, p.yx2, p.yy2, p.yz2);
     };
-    auto cval = [&](T ctr, T bv, T lap) {
-        return FIRST ? taylor_first(ctr, lap, p.coefC) : leapfrog(ctr, bv, lap, p.coefC);
+    auto coefL = [&](int L) { return L == 0 ? p.coefC : (L == 1 ? p.coefD : p.coefE); };
+    auto leap = [&](int L, T ctr, T u2, T l) {
+        if constexpr (FM) return leapfrog_fma(ctr, u2, l);
+        else return leapfrog(ctr, u2, l, coefL(L));
+    };
+    auto incr = [&](int L, T dprev, T l) {  // increment form: d_new = d_prev + coef*lap
+        if constexpr (FM) return dprev + l;
+        else return delta_incr(dprev, l, coefL(L));
+    };
+    auto scaled = [&](int L, T l) {  // coef*lap (FIRST increment: d = coef*lap)
+        if constexpr (FM) return l;
+        else return coefL(L) * l;
+    };
+    auto lapA = [&](int H, int y, int x, T ctr, T xm, T xp) {
+        return lap(0, ctr, xm, xp, ldsA[H][y - 1][x], ldsA[H][y + 1][x], ldsA[H][y][x - 1], ldsA[H][y][x + 1]);
+    };
+    auto cval = [&](T ctr, T bv, T l) {
+        if constexpr (FM) return FIRST ? ctr + l : leapfrog_fma(ctr, bv, l);
+        else return FIRST ? taylor_first(ctr, l, p.coefC) : leapfrog(ctr, bv, l, p.coefC);
     };
     // errors and finiteness sum of the own nodes of plane i of a layer (values v[r]); the
     // uniform error-plane test sits outside the per-lane row masks (a scalar branch)
@@ -338,7 +362,7 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WP
             const int y = 3 + w * R + r, x = 3 + lane;
             const T lap = lapA(H0, y, x, a[S1][r], xpA[r], xnA[r]);
             if constexpr (DELTA) {
-                const T dv = FIRST ? p.coefC * lap : delta_incr(bb[H0][r], lap, p.coefC);
+                const T dv = FIRST ? scaled(0, lap) : incr(0, bb[H0][r], lap);
                 dm[H0][r] = ocd[r] ? dv : T(0);
                 c[S0][r] = ocd[r] ? a[S1][r] + dv : T(0);  // FIRST: = taylor_first
             } else {
@@ -352,7 +376,7 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WP
                 const T lap = lapA(H0, ry[s], rx[s], ra[s][S1], rxp[s], rxn[s]);
                 T cv;
                 if constexpr (DELTA) {
-                    const T dv = FIRST ? p.coefC * lap : delta_incr(rb[s][H0], lap, p.coefC);
+                    const T dv = FIRST ? scaled(0, lap) : incr(0, rb[s][H0], lap);
                     rdm[s][H0] = rcd[s] ? dv : T(0);
                     cv = rcd[s] ? ra[s][S1] + dv : T(0);
                 } else {
@@ -387,15 +411,14 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WP
 #pragma unroll
             for (int r = 0; r < R; ++r) {
                 const int y = 2 + w * R + r, x = 2 + lane;  // C tile coordinates
-                const T lap = laplace7_cr(c[S3][r], cpx[r], cnx[r], ldsC[H1][y - 1][x],
-                                          ldsC[H1][y + 1][x], ldsC[H1][y][x - 1], ldsC[H1][y][x + 1],
-                                          p.hx2, p.hy2, p.hz2, p.yx2, p.yy2, p.yz2);
+                const T l = lap(1, c[S3][r], cpx[r], cnx[r], ldsC[H1][y - 1][x], ldsC[H1][y + 1][x],
+                                ldsC[H1][y][x - 1], ldsC[H1][y][x + 1]);
                 if constexpr (DELTA) {
-                    const T d1 = delta_incr(dm[H1][r], lap, p.coefD);  // d^{m+1}
+                    const T d1 = incr(1, dm[H1][r], l);  // d^{m+1}
                     dm1[H0][r] = ocd[r] ? d1 : T(0);
                     d[S0][r] = ocd[r] ? c[S3][r] + d1 : T(0);
                 } else {
-                    d[S0][r] = ocd[r] ? leapfrog(c[S3][r], a[S0][r], lap, p.coefD) : T(0);
+                    d[S0][r] = ocd[r] ? leap(1, c[S3][r], a[S0][r], l) : T(0);
                 }
                 ldsD[H0][y - 1][x - 1] = d[S0][r];
             }
@@ -403,13 +426,12 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WP
             for (int s = 0; s < RP; ++s) {
                 if (rg[s] == 1) {
                     const int y = ry[s] - 1, x = rx[s] - 1;
-                    const T lap = laplace7_cr(rc[s][S3], rcp[s], rcn[s], ldsC[H1][y - 1][x],
-                                              ldsC[H1][y + 1][x], ldsC[H1][y][x - 1], ldsC[H1][y][x + 1],
-                                              p.hx2, p.hy2, p.hz2, p.yx2, p.yy2, p.yz2);
+                    const T l = lap(1, rc[s][S3], rcp[s], rcn[s], ldsC[H1][y - 1][x], ldsC[H1][y + 1][x],
+                                    ldsC[H1][y][x - 1], ldsC[H1][y][x + 1]);
                     if constexpr (DELTA)
-                        ldsD[H0][y - 1][x - 1] = rcd[s] ? rc[s][S3] + delta_incr(rdm[s][H1], lap, p.coefD) : T(0);
+                        ldsD[H0][y - 1][x - 1] = rcd[s] ? rc[s][S3] + incr(1, rdm[s][H1], l) : T(0);
                     else
-                        ldsD[H0][y - 1][x - 1] = rcd[s] ? leapfrog(rc[s][S3], ra[s][S0], lap, p.coefD) : T(0);
+                        ldsD[H0][y - 1][x - 1] = rcd[s] ? leap(1, rc[s][S3], ra[s][S0], l) : T(0);
                 }
             }
             if (id >= ib && id <= ie) {
@@ -438,14 +460,13 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WP
 #pragma unroll
             for (int r = 0; r < R; ++r) {
                 const int y = 1 + w * R + r, x = 1 + lane;  // D tile coordinates
-                const T lap = laplace7_cr(d[S3][r], d[S2][r], d[S0][r], ldsD[H1][y - 1][x],
-                                          ldsD[H1][y + 1][x], ldsD[H1][y][x - 1], ldsD[H1][y][x + 1],
-                                          p.hx2, p.hy2, p.hz2, p.yx2, p.yy2, p.yz2);
+                const T l = lap(2, d[S3][r], d[S2][r], d[S0][r], ldsD[H1][y - 1][x], ldsD[H1][y + 1][x],
+                                ldsD[H1][y][x - 1], ldsD[H1][y][x + 1]);
                 if constexpr (DELTA) {
-                    dm1[H1][r] = delta_incr(dm1[H1][r], lap, p.coefE);  // d^{m+2}
+                    dm1[H1][r] = incr(2, dm1[H1][r], l);  // d^{m+2}
                     ev[r] = d[S3][r] + dm1[H1][r];
                 } else {
-                    ev[r] = leapfrog(d[S3][r], c[S2][r], lap, p.coefE);
+                    ev[r] = leap(2, d[S3][r], c[S2][r], l);
                 }
             }
             if constexpr (DELTA) {
@@ -517,9 +538,10 @@ struct SeamCParams {
     int sj, jmin, jmax, kmin, kmax;
     int cj0, cj1, ck0, ck1;
     T hx2, hy2, hz2, yx2, yy2, yz2, coef;
+    T fc[3];  // --math fma: coef/h^2 per axis
 };
 
-template <class T, bool FIRST, bool DELTA>
+template <class T, bool FIRST, bool DELTA, bool FM>
 __global__ void __launch_bounds__(kThreads) k_seam_c(const SeamCParams<T> p) {
     const SeamCOp<T> o = p.op[blockIdx.y];
     const int ktiles = (p.kmax - p.kmin - 1 + kTK - 1) / kTK;
@@ -530,18 +552,35 @@ __global__ void __launch_bounds__(kThreads) k_seam_c(const SeamCParams<T> p) {
     T v = T(0);
     if (j >= p.cj0 && j <= p.cj1 && k >= p.ck0 && k <= p.ck1) {
         const T a = o.Ac[c];
-        const T lap = laplace7_cr(a, o.Am[c], o.Ap[c], o.Ac[c - p.sj], o.Ac[c + p.sj], o.Ac[c - 1],
-                                  o.Ac[c + 1], p.hx2, p.hy2, p.hz2, p.yx2, p.yy2, p.yz2);
-        if constexpr (DELTA)  // Bc = d^{m-1}
-            v = FIRST ? a + p.coef * lap : a + delta_incr(o.Bc[c], lap, p.coef);
-        else
-            v = FIRST ? taylor_first(a, lap, p.coef) : leapfrog(a, o.Bc[c], lap, p.coef);
+        if constexpr (FM) {  // as the sweep's FM instantiation, so the seam C is the sweep's C
+            const T l = coef_lap_fma(a, o.Am[c], o.Ap[c], o.Ac[c - p.sj], o.Ac[c + p.sj], o.Ac[c - 1], o.Ac[c + 1],
+                                     p.fc[0], p.fc[1], p.fc[2]);
+            if constexpr (DELTA)
+                v = FIRST ? a + l : a + (o.Bc[c] + l);
+            else
+                v = FIRST ? a + l : leapfrog_fma(a, o.Bc[c], l);
+        } else {
+            const T lap = laplace7_cr(a, o.Am[c], o.Ap[c], o.Ac[c - p.sj], o.Ac[c + p.sj], o.Ac[c - 1],
+                                      o.Ac[c + 1], p.hx2, p.hy2, p.hz2, p.yx2, p.yy2, p.yz2);
+            if constexpr (DELTA)  // Bc = d^{m-1}
+                v = FIRST ? a + p.coef * lap : a + delta_incr(o.Bc[c], lap, p.coef);
+            else
+                v = FIRST ? taylor_first(a, lap, p.coef) : leapfrog(a, o.Bc[c], lap, p.coef);
+        }
     }
     o.out[c] = v;
 }
 
 template <class T, bool F>
-static void (*tb3_kernel(int rows, int waves))(const Tb3Params<T>) {
+static void (*tb3_kernel(int rows, int waves, bool fm = false))(const Tb3Params<T>) {
+    if (fm) {  // --math fma: the main tile shapes
+        switch (rows * 100 + waves) {
+            case 208: return k_tb3<T, F, 2, 8, false, true>;
+            case 108: return k_tb3<T, F, 1, 8, false, true>;
+            case 116: return k_tb3<T, F, 1, 16, false, true>;
+            default: return nullptr;
+        }
+    }
     switch (rows * 100 + waves) {
         case 404: return k_tb3<T, F, 4, 4>;
         case 208: return k_tb3<T, F, 2, 8>;
@@ -557,26 +596,36 @@ static void (*tb3_kernel(int rows, int waves))(const Tb3Params<T>) {
 // increment form: the 16-row and 1-row tiles (fp32 delta auto = r2w8: 537k vs tb2r2w8 520k Mpts/s
 // at N=512, profiles/tb3_diet_r2.txt)
 template <class T, bool F>
-static void (*tb3_delta_kernel(int rows, int waves))(const Tb3Params<T>) {
-    switch (rows * 100 + waves) {
+static void (*tb3_delta_kernel(int rows, int waves, bool fm = false))(const Tb3Params<T>) {
+    switch (rows * 100 + waves + (fm ? 10000 : 0)) {
         case 208: return k_tb3<T, F, 2, 8, true>;
         case 108: return k_tb3<T, F, 1, 8, true>;
+        case 10208: return k_tb3<T, F, 2, 8, true, true>;
+        case 10108: return k_tb3<T, F, 1, 8, true, true>;
         default: return nullptr;
     }
 }
 
-bool tb3_supported(int rows, int waves) { return tb3_kernel<double, false>(rows, waves) != nullptr; }
-bool tb3_delta_supported(int rows, int waves) { return tb3_delta_kernel<double, false>(rows, waves) != nullptr; }
+bool tb3_supported(int rows, int waves, bool fm) { return tb3_kernel<double, false>(rows, waves, fm) != nullptr; }
+bool tb3_delta_supported(int rows, int waves, bool fm) {
+    return tb3_delta_kernel<double, false>(rows, waves, fm) != nullptr;
+}
+
+// coef/h^2 of one layer for the FMA form
+template <class T>
+static void fma_coefs(const StepCoefs& c, T out[3]) {
+    out[0] = T(c.coef / c.hx2), out[1] = T(c.coef / c.hy2), out[2] = T(c.coef / c.hz2);
+}
 
 template <class T>
-void launch_tb3(int rows, int waves, bool delta, bool first, const T* A, const T* B, T* D, T* E,
+void launch_tb3(int rows, int waves, bool delta, bool fm, bool first, const T* A, const T* B, T* D, T* E,
                 const GridView& gv, const Box* boxes, int nbox, const Box& cdom, int ei0, int ei1,
                 const Wrap& wrapD, const Wrap& wrapE, const SeamPartners<T>& seam, const T* txy,
                 const T* tz, const StepCoefs& cC, const StepCoefs& cD,
                 const StepCoefs& cE, u64* errC, u64* errD, u64* errE, int chunk, hipStream_t s) {
     W3D_REQUIRE(gv.G >= 3, "three-layer temporal blocking needs ghost depth >= 3");
-    W3D_REQUIRE(tb3_supported(rows, waves), "tb3: unsupported rows x waves");
-    W3D_REQUIRE(!delta || tb3_delta_supported(rows, waves), "tb3 increment form: tiles r2w8, r1w8 only");
+    W3D_REQUIRE(tb3_supported(rows, waves, fm && !delta), "tb3: unsupported rows x waves (x --math fma)");
+    W3D_REQUIRE(!delta || tb3_delta_supported(rows, waves, fm), "tb3 increment form: tiles r2w8, r1w8 only");
     W3D_REQUIRE(nbox >= 1 && nbox <= kMaxBoxes, "bad box count");
     W3D_REQUIRE(gv.si * i64(sizeof(T)) < (i64(1) << 31), "tb3: plane larger than 2 GiB");
     Tb3Params<T> p{};
@@ -605,6 +654,7 @@ void launch_tb3(int rows, int waves, bool delta, bool first, const T* A, const T
     p.yx2 = T(1) / T(cC.hx2), p.yy2 = T(1) / T(cC.hy2), p.yz2 = T(1) / T(cC.hz2);
     p.coefC = T(cC.coef), p.coefD = T(cD.coef), p.coefE = T(cE.coef);
     p.ctC = T(cC.ct), p.ctD = T(cD.ct), p.ctE = T(cE.ct);
+    fma_coefs(cC, p.fc[0]), fma_coefs(cD, p.fc[1]), fma_coefs(cE, p.fc[2]);
     p.errC = errC, p.errD = errD, p.errE = errE;
     const int TJ = waves * rows;
     int nb = 0, total = 0;
@@ -630,14 +680,14 @@ void launch_tb3(int rows, int waves, bool delta, bool first, const T* A, const T
     }
     p.nbox = nb;
     if (nb == 0) return;
-    auto kern = delta ? (first ? tb3_delta_kernel<T, true>(rows, waves) : tb3_delta_kernel<T, false>(rows, waves))
-                      : (first ? tb3_kernel<T, true>(rows, waves) : tb3_kernel<T, false>(rows, waves));
+    auto kern = delta ? (first ? tb3_delta_kernel<T, true>(rows, waves, fm) : tb3_delta_kernel<T, false>(rows, waves, fm))
+                      : (first ? tb3_kernel<T, true>(rows, waves, fm) : tb3_kernel<T, false>(rows, waves, fm));
     hipLaunchKernelGGL(kern, dim3(total), dim3(waves * 64), 0, s, p);
     HIP_OK(hipGetLastError());
 }
 
 template <class T>
-void launch_seam_c(bool first, bool delta, const SeamCPlane<T>* ops, int nops, const GridView& gv,
+void launch_seam_c(bool first, bool delta, bool fm, const SeamCPlane<T>* ops, int nops, const GridView& gv,
                    const Box& cdom, const StepCoefs& cC, hipStream_t s) {
     W3D_REQUIRE(nops >= 0 && nops <= 2, "seam C: at most two planes");
     if (nops == 0) return;
@@ -650,20 +700,24 @@ void launch_seam_c(bool first, bool delta, const SeamCPlane<T>* ops, int nops, c
     p.hx2 = T(cC.hx2), p.hy2 = T(cC.hy2), p.hz2 = T(cC.hz2);
     p.yx2 = T(1) / T(cC.hx2), p.yy2 = T(1) / T(cC.hy2), p.yz2 = T(1) / T(cC.hz2);
     p.coef = T(cC.coef);
+    fma_coefs(cC, p.fc);
     const int rows = p.jmax - p.jmin - 1, ktiles = cdiv(p.kmax - p.kmin - 1, kTK);
     const dim3 grid(cdiv(rows, kWaves) * ktiles, nops);
-    void (*kern)(const SeamCParams<T>) = delta ? (first ? k_seam_c<T, true, true> : k_seam_c<T, false, true>)
-                                               : (first ? k_seam_c<T, true, false> : k_seam_c<T, false, false>);
+    void (*kern)(const SeamCParams<T>) =
+        fm ? (delta ? (first ? k_seam_c<T, true, true, true> : k_seam_c<T, false, true, true>)
+                    : (first ? k_seam_c<T, true, false, true> : k_seam_c<T, false, false, true>))
+           : (delta ? (first ? k_seam_c<T, true, true, false> : k_seam_c<T, false, true, false>)
+                    : (first ? k_seam_c<T, true, false, false> : k_seam_c<T, false, false, false>));
     hipLaunchKernelGGL(kern, grid, dim3(kThreads), 0, s, p);
     HIP_OK(hipGetLastError());
 }
-template void launch_seam_c<double>(bool, bool, const SeamCPlane<double>*, int, const GridView&, const Box&,
+template void launch_seam_c<double>(bool, bool, bool, const SeamCPlane<double>*, int, const GridView&, const Box&,
                                     const StepCoefs&, hipStream_t);
-template void launch_seam_c<float>(bool, bool, const SeamCPlane<float>*, int, const GridView&, const Box&,
+template void launch_seam_c<float>(bool, bool, bool, const SeamCPlane<float>*, int, const GridView&, const Box&,
                                    const StepCoefs&, hipStream_t);
 
 #define W3D_TB3_INST(T)                                                                       \
-    template void launch_tb3<T>(int, int, bool, bool, const T*, const T*, T*, T*, const GridView&,  \
+    template void launch_tb3<T>(int, int, bool, bool, bool, const T*, const T*, T*, T*, const GridView&, \
                                 const Box*, int, const Box&, int, int, const Wrap&,           \
                                 const Wrap&, const SeamPartners<T>&, const T*,                \
                                 const T*, const StepCoefs&, const StepCoefs&,                 \

@@ -95,7 +95,7 @@ std::string json_summary(const Config& c, const RunResult& r) {
     s << "{\"N\": " << r.N << ", \"timesteps\": " << r.K << ", \"nprocs\": " << r.nprocs
       << ", \"dims\": [" << r.dims[0] << ", " << r.dims[1] << ", " << r.dims[2] << "]"
       << ", \"dtype\": \"" << dtype_name(r.dtype) << "\", \"backend\": \"" << r.backend
-      << "\", \"kernel\": \"" << r.kernel << "\", \"scheme\": \"" << r.scheme
+      << "\", \"kernel\": \"" << r.kernel << "\", \"scheme\": \"" << r.scheme << "\", \"math\": \"" << r.math
       << "\", \"transport\": \"" << r.transport << "\""
       << ", \"overlap\": " << (r.overlap ? "true" : "false") << ", \"overlap_mode\": \"" << r.overlap_mode
       << "\", \"overlap_trial_ms\": [" << jnum(r.overlap_trial_ms[0]) << ", " << jnum(r.overlap_trial_ms[1]) << "]"

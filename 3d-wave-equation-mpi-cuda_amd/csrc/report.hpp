@@ -26,6 +26,7 @@ struct RunResult {
     std::string backend;     // "hip" | "cpu"
     std::string kernel;      // stencil variant actually used
     std::string scheme = "leapfrog";  // time stepping: "leapfrog" | "delta" (increment form)
+    std::string math = "exact";       // stencil arithmetic: "exact" (reference order) | "fma"
     std::string transport;   // "self" | "loopback" | "rccl" | "external"
     double courant = 0;
     std::vector<double> max_abs, max_rel;  // per layer, max over all ranks

@@ -139,6 +139,25 @@ W3D_HD void accumulate_error_fast(T u, T f, T& mabs, T& mrel) {
     if (er > mrel) mrel = er;
 }
 
+// ---- FMA form (--math fma): the same scheme with coef/h^2 folded into three constants ------
+// coef*lap = cx*((xm + xp) - 2c) + cy*(...) + cz*(...), cd = coef/hd^2: every second difference
+// is still formed before it is scaled (no loss of the small h^2 u'' term, so fp32 keeps its
+// accuracy), 8 FP operations instead of the exact form's ~19 (three correctly rounded
+// divisions), rounded differently from the reference CPU programs — as nvcc's default FMA
+// contraction rounds the reference's own CUDA kernel (cuda_sol_kernels.cu:36-38) differently.
+template <class T>
+W3D_HD T coef_lap_fma(T c, T xm, T xp, T ym, T yp, T zm, T zp, T cx, T cy, T cz) {
+    const T sx = fma_t(T(-2), c, xm + xp);
+    const T sy = fma_t(T(-2), c, ym + yp);
+    const T sz = fma_t(T(-2), c, zm + zp);
+    return fma_t(cx, sx, fma_t(cy, sy, cz * sz));
+}
+// leapfrog with a pre-scaled Laplacian l = coef*lap: (2c - u2) + l
+template <class T>
+W3D_HD T leapfrog_fma(T c, T u2, T l) {
+    return fma_t(T(2), c, -u2) + l;
+}
+
 // True for NaN and +-Inf (x - x is NaN exactly for those).
 template <class T>
 W3D_HD bool nonfinite(T x) {

@@ -206,21 +206,22 @@ def tb_sweep(A, B, C, D, boxes, *, first: bool, cdom, err_i, tx, ty, tz, coefs_c
 
 def tb3_sweep(A, B, D, E, boxes, *, first: bool, cdom, err_i, tx, ty, tz, coefs_c, coefs_d,
               coefs_e, err_c, err_d, err_e, rows: int = 2, waves: int = 8, chunk: int = 0,
-              ghost: int = 3) -> None:
-    """One three-layer sweep (k_tb3): C = u^m (errors only), D = u^{m+1}, E = u^{m+2}."""
+              ghost: int = 3, fma: bool = False) -> None:
+    """One three-layer sweep (k_tb3): C = u^m (errors only), D = u^{m+1}, E = u^{m+2}.
+    ``fma``: the --math fma instantiation (coef/h^2 folded; not bitwise with the exact form)."""
     gv = _check_grid_g(ghost, A, B, D, E)
     if ghost < 3:
         raise ValueError("k_tb3 needs ghost depth >= 3")
     if isinstance(boxes[0], int):
         boxes = [boxes]
     bl = [_check_box_g(b, gv) for b in boxes]
-    if not _C().tb_supported(3, rows, waves):
-        raise ValueError(f"unsupported tile rows={rows} waves={waves}")
+    if not _C().tb_supported(3, rows, waves, fm=bool(fma)):
+        raise ValueError(f"unsupported tile rows={rows} waves={waves} fma={fma}")
     for t in (tx, ty, tz):
         if not t.is_cuda or t.dtype != A.dtype or t.numel() < max(gv[:3]):
             raise ValueError("analytic tables must be device tensors covering the grid")
     fn = getattr(_C(), "k_tb3_" + _sfx(A))
-    fn(int(rows), int(waves), bool(first), A.data_ptr(), B.data_ptr(), D.data_ptr(), E.data_ptr(),
+    fn(int(rows), int(waves), bool(fma), bool(first), A.data_ptr(), B.data_ptr(), D.data_ptr(), E.data_ptr(),
        gv, bl, [int(v) for v in cdom], int(err_i[0]), int(err_i[1]), tx.data_ptr(),
        ty.data_ptr(), tz.data_ptr(), [float(c) for c in coefs_c], [float(c) for c in coefs_d],
        [float(c) for c in coefs_e], err_c.data_ptr(), err_d.data_ptr(), err_e.data_ptr(),
