@@ -204,3 +204,37 @@ def test_tb2_delta_sweep_matches_reference(C, dtype, first, rows, waves, kw, cas
         s = _sl(boxes[0], G)
         _check_err(errC, Cf[s], boxes[0], ei, tx, ty, tz, CT[0], dtype)
         _check_err(errD, gD[s], boxes[0], ei, tx, ty, tz, CT[1], dtype)
+
+
+@pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
+@pytest.mark.parametrize("first", [False, True])
+@pytest.mark.parametrize("rows,waves", [(2, 8), (1, 16), (1, 8)])
+@pytest.mark.parametrize("case", [0, 2, 3])
+def test_tb3_fma_sweep_close_to_reference(C, dtype, first, rows, waves, case):
+    """--math fma: the same three-layer sweep with coef/h^2 folded into FMAs. Not bitwise (the
+    reference's operation order is not kept), so within a few ulps of the chained oracle."""
+    from wave3d.ops import kernels, reference
+
+    (X, Y, Z), boxes, cdom, chunk = CASES[case]
+    G = 3
+    shape = (X + 2 * G, Y + 2 * G, Z + 2 * G)
+    A, B = _rand(shape, dtype, 4), _rand(shape, dtype, 5)
+    tx, ty, tz = _tables(max(shape), dtype, 6)
+    dD, dE = torch.full(shape, -7.0, dtype=dtype, device=DEV), torch.full(shape, -9.0, dtype=dtype, device=DEV)
+    errs = [kernels.new_err(1) for _ in range(3)]
+    ei = (min(b[0] for b in boxes), max(b[1] for b in boxes))
+    co = [(*COEF.values(), COEFS[q], CT[q]) for q in range(3)]
+    kernels.tb3_sweep(A.to(DEV), B.to(DEV), dD, dE, boxes, first=first, cdom=cdom, err_i=ei,
+                      tx=tx.to(DEV), ty=ty.to(DEV), tz=tz.to(DEV), coefs_c=co[0], coefs_d=co[1],
+                      coefs_e=co[2], err_c=errs[0], err_d=errs[1], err_e=errs[2], rows=rows,
+                      waves=waves, chunk=chunk, fma=True)
+    torch.cuda.synchronize()
+    h = {k: float(v) for k, v in COEF.items()}
+    Cf, Df, Ef = reference.chained_layers(A.double(), B.double(), 3, first=first, mask=_mask(shape, G, cdom),
+                                          coefs=list(COEFS), **h)
+    tol = dict(rtol=1e-12, atol=1e-12) if dtype == torch.float64 else dict(rtol=2e-5, atol=2e-5)
+    gD, gE = dD.cpu(), dE.cpu()
+    for b in boxes:
+        s = _sl(b, G)
+        torch.testing.assert_close(gD[s].double(), Df[s], **tol)
+        torch.testing.assert_close(gE[s].double(), Ef[s], **tol)
