@@ -213,7 +213,7 @@ void k_tb2_dense(int rows, int waves, int nwk, bool delta, bool first, uintptr_t
     if (hipMalloc(&txy, txy_elems(v.X, v.Y) * sizeof(T)) != hipSuccess) throw Error("k_tb2: hipMalloc failed");
     try {
         launch_txy<T>(txy, P<T>(tx), P<T>(ty), v.X, v.Y, s);
-        launch_tb2<T>(rows, waves, 0, nwk, delta, first, P<T>(A) + o, P<T>(B) + o, P<T>(Cc) + o, P<T>(D) + o, v,
+        launch_tb2<T>(rows, waves, 0, nwk, delta, false, first, P<T>(A) + o, P<T>(B) + o, P<T>(Cc) + o, P<T>(D) + o, v,
                       bx.data(), int(bx.size()), tobox(cdom), ei0, ei1, towrap(wrapC), towrap(wrapD),
                       SeamAlias<T>{}, txy, P<T>(tz), tocoefs(cC), tocoefs(cD),
                       P<u64>(errC), P<u64>(errD), chunk, s);

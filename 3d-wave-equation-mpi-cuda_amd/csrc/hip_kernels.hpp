@@ -189,8 +189,10 @@ bool tb2_supported(int rows, int waves, int occ = 0, int nwk = 1);
 // planes), D receives u^{m+1}; u^m is formed in registers for its errors only.
 bool tb2_delta_supported(int rows, int waves, int nwk = 1);
 // `txy` = the sx*sy product table of launch_txy (X, Y of gv).
+// fm: the --math fma instantiations (r2w8, r2w4; increment form r2w8)
+bool tb2_fma_supported(int rows, int waves, int nwk, bool delta);
 template <class T>
-void launch_tb2(int rows, int waves, int occ, int nwk, bool delta, bool first, const T* A, const T* B, T* C, T* D, const GridView& gv,
+void launch_tb2(int rows, int waves, int occ, int nwk, bool delta, bool fm, bool first, const T* A, const T* B, T* C, T* D, const GridView& gv,
                 const Box* boxes, int nbox, const Box& cdom, int ei0, int ei1, const Wrap& wrapC,
                 const Wrap& wrapD, const SeamAlias<T>& alias, const T* txy, const T* tz,
                 const StepCoefs& cC, const StepCoefs& cD, u64* errC, u64* errD,

@@ -133,9 +133,11 @@ public:
         G_ = lay.G;
         L_ = lay.L;
         for (int a = 0; a < 3; ++a) cfg_.dims[a] = lay.dims[a];
-        W3D_REQUIRE(!c.fma || (tb_ && tbd_ == 3 && (c.delta ? tb3_delta_supported(tb_rows_, tb_waves_, true)
-                                                              : tb3_supported(tb_rows_, tb_waves_, true))),
-                    "--math fma needs a three-layer kernel with an fma instantiation (tb3, tb3r1w8, tb3r1w16)");
+        W3D_REQUIRE(!c.fma || (tb_ && (tbd_ == 3 ? (c.delta ? tb3_delta_supported(tb_rows_, tb_waves_, true)
+                                                            : tb3_supported(tb_rows_, tb_waves_, true))
+                                                 : tb_occ_ == 0 && tb2_fma_supported(tb_rows_, tb_waves_, tb_nwk_, c.delta))),
+                    "--math fma needs a temporal-blocking kernel with an fma instantiation (tb3, tb3r1w8, "
+                    "tb3r1w16, tb2r2w8, tb2)");
         W3D_REQUIRE(!tb_ || (tbd_ == 3 ? tb3_supported(tb_rows_, tb_waves_)
                                         : tb2_supported(tb_rows_, tb_waves_, tb_occ_, tb_nwk_)),
                     "wave3d: unknown kernel variant " + c.kernel);
@@ -801,7 +803,10 @@ private:
         // two-layer tails of a tb3 run whose tile has no tb2 instantiation (1-row tiles) use
         // the default tb2 tile
         const bool own = tb2_supported(tb_rows_, tb_waves_, tb_occ_, tb_nwk_);
-        launch_tb2<T>(own ? tb_rows_ : 2, own ? tb_waves_ : 8, own ? tb_occ_ : 0, own ? tb_nwk_ : 1, cfg_.delta, m == 1, A, B, R.g[lvl(m)], R.g[lvl(m + 1)], R.gv, boxes, nbox,
+        // (--math fma tails of a tb3 run: the r2w8 fma instantiation)
+        launch_tb2<T>(own ? tb_rows_ : 2, own ? tb_waves_ : 8, own ? tb_occ_ : 0, own ? tb_nwk_ : 1, cfg_.delta,
+                      cfg_.fma && tb2_fma_supported(own ? tb_rows_ : 2, own ? tb_waves_ : 8, own ? tb_nwk_ : 1, cfg_.delta),
+                      m == 1, A, B, R.g[lvl(m)], R.g[lvl(m + 1)], R.gv, boxes, nbox,
                       R.cdom, R.error.i0, R.error.i1, R.wrap, R.wrap2, al, R.txy, R.tz,
                       coefs(m), coefs(m + 1), R.err + size_t(m) * kSlotsPerLayer,
                       R.err + size_t(m + 1) * kSlotsPerLayer, cfg_.chunk, s);

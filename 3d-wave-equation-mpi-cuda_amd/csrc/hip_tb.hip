@@ -65,6 +65,7 @@ struct TbParams {
     const T* tz;
     T hx2, hy2, hz2, coefC, coefD, ctC, ctD;
     T yx2, yy2, yz2;  // RN(1/h^2): correctly rounded constant division
+    T fc[2][3];       // --math fma: coef/h^2 of layers C, D per axis
     u64* errC;
     u64* errD;
 };
@@ -88,8 +89,9 @@ struct TbParams {
 // kb+TK..kb+TK+1 sit in two 128-B lines owned by the k-neighbour tile, which runs on another
 // XCD, so they are fetched again from beyond L2 — the bulk of tb2's read surplus,
 // profiles/dram_bytes_r2.txt).
+// FM: --math fma (stencil_math coef_lap_fma), as k_tb3.
 template <class T, bool FIRST, int R, int NW, int WPE = 1, int ABL = 0, int OPT = 0, bool DELTA = false,
-          int NWK = 1>
+          int NWK = 1, bool FM = false>
 __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WPE, 8))) k_tb2(const TbParams<T> p) {
     static_assert(NW % NWK == 0, "waves along k must divide the workgroup");
     constexpr int NWJ = NW / NWK;
@@ -252,6 +254,30 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WP
     RelArg<T> mr1, mr2;
     T chk1 = T(0), chk2 = T(0);
 
+    // layer L (0 = C, 1 = D) arithmetic: exact Laplacian or (FM) coef*Laplacian, and the updates
+    auto lap = [&](int L, T ctr, T xm, T xp, T ym, T yp, T zm, T zp) {
+        if constexpr (FM)
+            return coef_lap_fma(ctr, xm, xp, ym, yp, zm, zp, p.fc[L][0], p.fc[L][1], p.fc[L][2]);
+        else
+            return laplace7_cr(ctr, xm, xp, ym, yp, zm, zp, p.hx2, p.hy2, p.hz2, p.yx2, p.yy2, p.yz2);
+    };
+    auto leap = [&](int L, T ctr, T u2, T l) {
+        if constexpr (FM) return leapfrog_fma(ctr, u2, l);
+        else return leapfrog(ctr, u2, l, L == 0 ? p.coefC : p.coefD);
+    };
+    auto first1 = [&](T ctr, T l) {
+        if constexpr (FM) return ctr + l;
+        else return taylor_first(ctr, l, p.coefC);
+    };
+    auto incr = [&](int L, T dprev, T l) {
+        if constexpr (FM) return dprev + l;
+        else return delta_incr(dprev, l, L == 0 ? p.coefC : p.coefD);
+    };
+    auto scaled = [&](T l) {
+        if constexpr (FM) return l;
+        else return p.coefC * l;
+    };
+
     // errors and finiteness sum of one own plane i of a layer (values v[r]); the uniform plane
     // test outside the per-lane row masks keeps it a scalar branch
     auto errors = [&](const T(&v)[R], const int i, const T ct, T& ma, RelArg<T>& mr, T& chk) {
@@ -336,30 +362,25 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WP
 #pragma unroll
         for (int r = 0; r < R; ++r) {
             const int ya = 2 + w * R + r, xa = 2 + kl;
-            const T lap = laplace7_cr(a[S1][r], xpA[r], xnA[r], ldsA[H0][ya - 1][xa],
-                                      ldsA[H0][ya + 1][xa], ldsA[H0][ya][xa - 1],
-                                      ldsA[H0][ya][xa + 1], p.hx2, p.hy2, p.hz2, p.yx2, p.yy2,
-                                      p.yz2);
+            const T l = lap(0, a[S1][r], xpA[r], xnA[r], ldsA[H0][ya - 1][xa], ldsA[H0][ya + 1][xa],
+                            ldsA[H0][ya][xa - 1], ldsA[H0][ya][xa + 1]);
             T cv;
             if constexpr (DELTA) {
-                const T dm = FIRST ? p.coefC * lap : delta_incr(bb[H0][r], lap, p.coefC);
+                const T dm = FIRST ? scaled(l) : incr(0, bb[H0][r], l);
                 dl[H0][r] = ocd[r] ? dm : T(0);
                 cv = a[S1][r] + dm;  // FIRST: = taylor_first (u0 + coef_first*lap)
             } else {
-                cv = FIRST ? taylor_first(a[S1][r], lap, p.coefC)
-                           : leapfrog(a[S1][r], bb[H0][r], lap, p.coefC);
+                cv = FIRST ? first1(a[S1][r], l) : leap(0, a[S1][r], bb[H0][r], l);
             }
             c[S0][r] = ocd[r] ? cv : T(0);
             ldsC[H0][1 + w * R + r][1 + kl] = c[S0][r];
         }
         if (ron) {
             const int ya = rj - jt + 2, xa = rk - kb + 2;
-            const T lap = laplace7_cr(ra[S1], rxp, rxn, ldsA[H0][ya - 1][xa], ldsA[H0][ya + 1][xa],
-                                      ldsA[H0][ya][xa - 1], ldsA[H0][ya][xa + 1], p.hx2, p.hy2,
-                                      p.hz2, p.yx2, p.yy2, p.yz2);
-            const T cv = FIRST ? taylor_first(ra[S1], lap, p.coefC)
-                               : (DELTA ? ra[S1] + delta_incr(rb[H0], lap, p.coefC)
-                                        : leapfrog(ra[S1], rb[H0], lap, p.coefC));
+            const T l = lap(0, ra[S1], rxp, rxn, ldsA[H0][ya - 1][xa], ldsA[H0][ya + 1][xa],
+                            ldsA[H0][ya][xa - 1], ldsA[H0][ya][xa + 1]);
+            const T cv = FIRST ? first1(ra[S1], l)
+                               : (DELTA ? ra[S1] + incr(0, rb[H0], l) : leap(0, ra[S1], rb[H0], l));
             ldsC[H0][ya - 1][xa - 1] = rcd ? cv : T(0);
         }
 
@@ -389,15 +410,13 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WP
 #pragma unroll
             for (int r = 0; r < R; ++r) {
                 const int yc = 1 + w * R + r, xc = 1 + kl;
-                const T lap = laplace7_cr(c[S3][r], c[S2][r], c[S0][r], ldsC[H1][yc - 1][xc],
-                                          ldsC[H1][yc + 1][xc], ldsC[H1][yc][xc - 1],
-                                          ldsC[H1][yc][xc + 1], p.hx2, p.hy2, p.hz2, p.yx2,
-                                          p.yy2, p.yz2);
+                const T l = lap(1, c[S3][r], c[S2][r], c[S0][r], ldsC[H1][yc - 1][xc], ldsC[H1][yc + 1][xc],
+                                ldsC[H1][yc][xc - 1], ldsC[H1][yc][xc + 1]);
                 if constexpr (DELTA) {
-                    dl[H1][r] = delta_incr(dl[H1][r], lap, p.coefD);  // d^{m+1}
+                    dl[H1][r] = incr(1, dl[H1][r], l);  // d^{m+1}
                     dv[r] = c[S3][r] + dl[H1][r];
                 } else {
-                    dv[r] = leapfrog(c[S3][r], a[S0][r], lap, p.coefD);
+                    dv[r] = leap(1, c[S3][r], a[S0][r], l);
                 }
             }
             const auto rd = prs(p.D, id, pbytes);
@@ -458,6 +477,20 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WP
 
 // increment form: the main tile shapes only
 template <class T, bool F>
+static void (*tb_fma_kernel(int rows, int waves, int nwk, bool delta))(const TbParams<T>) {
+    switch (rows * 100 + waves * 10 + nwk + (delta ? 10000 : 0)) {
+        case 281: return k_tb2<T, F, 2, 8, 1, 0, 0, false, 1, true>;
+        case 241: return k_tb2<T, F, 2, 4, 1, 0, 0, false, 1, true>;
+        case 10281: return k_tb2<T, F, 2, 8, 1, 0, 0, true, 1, true>;
+        default: return nullptr;
+    }
+}
+
+bool tb2_fma_supported(int rows, int waves, int nwk, bool delta) {
+    return tb_fma_kernel<double, false>(rows, waves, nwk, delta) != nullptr;
+}
+
+template <class T, bool F>
 static void (*tb_delta_kernel(int rows, int waves, int nwk))(const TbParams<T>) {
     switch (rows * 100 + waves * 10 + nwk) {
         case 241: return k_tb2<T, F, 2, 4, 1, 0, 0, true>;
@@ -512,7 +545,7 @@ bool tb2_supported(int rows, int waves, int occ, int nwk) {
 }
 
 template <class T>
-void launch_tb2(int rows, int waves, int occ, int nwk, bool delta, bool first, const T* A, const T* B, T* C, T* D, const GridView& gv,
+void launch_tb2(int rows, int waves, int occ, int nwk, bool delta, bool fm, bool first, const T* A, const T* B, T* C, T* D, const GridView& gv,
                 const Box* boxes, int nbox, const Box& cdom, int ei0, int ei1, const Wrap& wrapC,
                 const Wrap& wrapD, const SeamAlias<T>& alias, const T* txy, const T* tz,
                 const StepCoefs& cC, const StepCoefs& cD, u64* errC, u64* errD,
@@ -521,6 +554,8 @@ void launch_tb2(int rows, int waves, int occ, int nwk, bool delta, bool first, c
     W3D_REQUIRE(tb2_supported(rows, waves, occ, nwk), "tb2: unsupported rows x waves x occupancy x k-waves");
     W3D_REQUIRE(!delta || (occ == 0 && tb2_delta_supported(rows, waves, nwk)),
                 "tb2 increment form: tiles r2w4, r2w8, r4w4, r2w8k2 only");
+    W3D_REQUIRE(!fm || (occ == 0 && tb2_fma_supported(rows, waves, nwk, delta)),
+                "tb2 --math fma: tiles r2w8, r2w4 (leapfrog), r2w8 (increment form) only");
     W3D_REQUIRE(nbox >= 1 && nbox <= kMaxBoxes, "bad box count");
     W3D_REQUIRE(gv.si * i64(sizeof(T)) < (i64(1) << 31), "tb2: plane larger than 2 GiB");
     TbParams<T> p{};
@@ -566,6 +601,10 @@ void launch_tb2(int rows, int waves, int occ, int nwk, bool delta, bool first, c
     p.yz2 = T(1) / T(cC.hz2);
     p.coefC = T(cC.coef);
     p.coefD = T(cD.coef);
+    for (int L = 0; L < 2; ++L) {
+        const StepCoefs& c = L ? cD : cC;
+        p.fc[L][0] = T(c.coef / c.hx2), p.fc[L][1] = T(c.coef / c.hy2), p.fc[L][2] = T(c.coef / c.hz2);
+    }
     p.ctC = T(cC.ct);
     p.ctD = T(cD.ct);
     p.errC = errC;
@@ -601,14 +640,15 @@ void launch_tb2(int rows, int waves, int occ, int nwk, bool delta, bool first, c
     }
     p.nbox = nb;
     if (nb == 0) return;
-    auto kern = delta ? (first ? tb_delta_kernel<T, true>(rows, waves, nwk) : tb_delta_kernel<T, false>(rows, waves, nwk))
+    auto kern = fm ? (first ? tb_fma_kernel<T, true>(rows, waves, nwk, delta) : tb_fma_kernel<T, false>(rows, waves, nwk, delta))
+              : delta ? (first ? tb_delta_kernel<T, true>(rows, waves, nwk) : tb_delta_kernel<T, false>(rows, waves, nwk))
                       : (first ? tb_kernel<T, true>(rows, waves, occ, nwk) : tb_kernel<T, false>(rows, waves, occ, nwk));
     hipLaunchKernelGGL(kern, dim3(total), dim3(waves * 64), 0, s, p);
     HIP_OK(hipGetLastError());
 }
 
 #define W3D_TB_INST(T)                                                                       \
-    template void launch_tb2<T>(int, int, int, int, bool, bool, const T*, const T*, T*, T*, const GridView&, \
+    template void launch_tb2<T>(int, int, int, int, bool, bool, bool, const T*, const T*, T*, T*, const GridView&, \
                                 const Box*, int, const Box&, int, int, const Wrap&,          \
                                 const Wrap&, const SeamAlias<T>&, const T*, const T*,        \
                                 const StepCoefs&, const StepCoefs&, u64*, u64*,              \

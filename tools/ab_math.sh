@@ -7,7 +7,7 @@ B=3d-wave-equation-mpi-cuda_amd/build/wave3d
 N=${N:-512}
 K=${K:-100}
 DT=${DT:-fp64}
-ARMS=${ARMS:-"tb2r2w8:exact tb3:exact tb3r1w8:exact tb3:fma tb3r1w8:fma tb3r1w16:fma"}
+ARMS=${ARMS:-"tb2r2w8:exact tb2r2w8:fma tb3:exact tb3r1w8:exact tb3:fma tb3r1w8:fma tb3r1w16:fma"}
 for rep in $(seq ${ROUNDS:-2}); do
   for arm in $ARMS; do
     k=${arm%%:*}; m=${arm##*:}
