@@ -92,17 +92,21 @@ def test_bench_plan_maps_gpu_counts_to_baseline_configs(C):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("n,N,dims", [(2, 512, [2, 1, 1]), (4, 1024, [2, 2, 1]), (8, 1024, [2, 2, 2])])
-def test_bench_gpu_multirank_plan_staged(n, N, dims):
+@pytest.mark.parametrize("n,N,dims,golden", [(2, 512, [2, 1, 1], 6.03381e-07), (4, 1024, [2, 2, 1], 8.04265e-08),
+                                             (8, 1024, [2, 2, 2], 8.04265e-08)])
+def test_bench_gpu_multirank_plan_staged(n, N, dims, golden):
     """The multi-GPU benchmark path end to end with n processes on one MI355X (staged device
-    transport; RCCL refuses duplicate GPUs): each n runs its BASELINE config and decomposition.
-    Few layers (unstable Courant number, plumbing only), so the L-inf is not checked."""
-    r = _bench(["--steps", "1", "--warmup", "0", "--timesteps", "6", "--transport", "staged",
-                "--shared-device"], nproc=n, timeout=600)
+    transport; RCCL refuses duplicate GPUs): each n runs its BASELINE config and decomposition
+    at the benchmark's K=100 and must reproduce the reference's golden L-inf; the halo plan is
+    verified at setup (halo_checked) and --overlap auto records both trial times."""
+    r = _bench(["--steps", "1", "--warmup", "1", "--transport", "staged", "--shared-device"], nproc=n,
+               timeout=900)
     assert r["n_gpus"] == n and r["config"]["N"] == N and r["config"]["dims"] == dims
     assert r["config"]["transport"] == "staged.gloo" and r["rccl_nranks"] is None
-    assert r["config"]["overlap"] is True and r["value"] > 0
-    assert r["timers_ms"]["exchange_ms"] > 0
+    assert r["config"]["timesteps"] == 100 and r["linf_golden"] == golden and r["linf_ok"] is True
+    assert r["halo_checked"] > 0 and r["value"] > 0
+    assert r["config"]["overlap_mode"] == "auto" and min(r["config"]["overlap_trial_ms"]) > 0
+    assert r["timers_ms"]["exchange_ms"] > 0 and r["timers_ms"]["comm_ms"] > 0
 
 
 @pytest.mark.gpu

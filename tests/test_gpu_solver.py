@@ -409,3 +409,38 @@ def test_overlap_concurrent_interior_bitwise(C, kernel, scheme, dims, K):
     assert r.extra["overlap"] is True and r.extra["overlap_interior"] > 0
     ref = _solve(p, backend="cpu", threads=8)
     assert r.max_abs == ref.max_abs and r.max_rel == ref.max_rel
+
+
+@pytest.mark.parametrize("kernel", ["tb3", "tb3r1w8", "tb2r2w8"])
+def test_fma_math_goldens(C, kernel):
+    """--math fma keeps the reference's printed error tables (6 significant digits) at N=32 and
+    the headline N=512 K=100 L-inf, though it is not bitwise with the exact form."""
+    import wave3d
+    from wave3d.utils import GOLDEN_N32_K20, GOLDEN_SPOTS
+
+    r = wave3d.WaveSolver(wave3d.WaveProblem(32, timesteps=20), "hip", kernel=kernel)
+    r.opts["math"] = "fma"
+    res = r.run()
+    assert res.extra["math"] == "fma" and _fmt(res) == GOLDEN_N32_K20
+    r = wave3d.WaveSolver(wave3d.WaveProblem(512, timesteps=100), "hip", kernel=kernel)
+    r.opts["math"] = "fma"
+    got = _fmt(r.run())
+    for layer, val in GOLDEN_SPOTS[(512, 100, "ref")].items():
+        assert got[layer] == val
+
+
+@pytest.mark.parametrize("kernel", ["tb3", "tb2r2w8"])
+@pytest.mark.parametrize("ranks,dims", [(8, [2, 2, 2]), (2, [2, 1, 1]), (4, [1, 2, 2])])
+def test_fma_math_decomposition_invariance(C, kernel, ranks, dims):
+    """Every node's FMA-form arithmetic is the same on any decomposition (rings recomputed with
+    the same operations, seam C planes by the same formula): bitwise equal to one rank."""
+    import wave3d
+
+    p = wave3d.WaveProblem(64, Lx=1.3, Ly="pi", Lz=2.0, timesteps=29, ic="shifted")
+    assert p.stable()
+    one = wave3d.WaveSolver(p, "hip", kernel=kernel)
+    one.opts["math"] = "fma"
+    many = wave3d.WaveSolver(p, "hip", kernel=kernel, ranks=ranks, dims=dims, overlap=True)
+    many.opts["math"] = "fma"
+    a, b = one.run(), many.run()
+    assert a.max_abs == b.max_abs and a.max_rel == b.max_rel
