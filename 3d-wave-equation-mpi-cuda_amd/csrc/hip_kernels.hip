@@ -724,6 +724,23 @@ void launch_txy(T* out, const T* tx, const T* ty, int X, int Y, hipStream_t s) {
 template void launch_txy<double>(double*, const double*, const double*, int, int, hipStream_t);
 template void launch_txy<float>(float*, const float*, const float*, int, int, hipStream_t);
 
+namespace {
+template <class T>
+__global__ void k_recip_abs(T* out, const T* in, size_t n) {
+    const size_t q = size_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (q < n) out[q] = T(1) / absval(in[q]);  // 1/0 = inf: |d| * inf as the reference's |d|/0
+}
+}  // namespace
+
+template <class T>
+void launch_recip_abs(T* out, const T* in, size_t n, hipStream_t s) {
+    if (n == 0) return;
+    hipLaunchKernelGGL(k_recip_abs<T>, dim3(unsigned((n + 255) / 256)), dim3(256), 0, s, out, in, n);
+    HIP_OK(hipGetLastError());
+}
+template void launch_recip_abs<double>(double*, const double*, size_t, hipStream_t);
+template void launch_recip_abs<float>(float*, const float*, size_t, hipStream_t);
+
 void launch_init_err(u64* err, int layers, hipStream_t s) {
     const int n = layers * 3;
     hipLaunchKernelGGL(k_init_err, dim3(cdiv(n, 256)), dim3(256), 0, s, err, n);

@@ -67,6 +67,8 @@ struct DevRank {
     size_t elems = 0;                                  // allocation per level
     T *tx = nullptr, *ty = nullptr, *tz = nullptr;
     T* txy = nullptr;  // sx*sy table of the temporal-blocking sweep (launch_txy)
+    T* rtxy = nullptr;  // --math fma: 1/|txy|, 1/|tz| (relative error without division)
+    T* rtz = nullptr;
     HaloPlan plan;
     std::vector<T*> sbuf, rbuf;  // y/z messages only (x messages live in the grid)
     u64* err = nullptr;          // (K+1) * kSlotsPerLayer
@@ -347,6 +349,12 @@ private:
             if (tb_) {
                 HIP_CHECK(hipMalloc(&R.txy, txy_elems(X, Y) * sizeof(T)));
                 launch_txy<T>(R.txy, R.tx, R.ty, X, Y, nullptr);
+                if (cfg_.fma) {
+                    HIP_CHECK(hipMalloc(&R.rtxy, txy_elems(X, Y) * sizeof(T)));
+                    HIP_CHECK(hipMalloc(&R.rtz, size_t(Z + 2) * sizeof(T)));
+                    launch_recip_abs<T>(R.rtxy, R.txy, txy_elems(X, Y), nullptr);
+                    launch_recip_abs<T>(R.rtz, R.tz, size_t(Z + 2), nullptr);
+                }
                 HIP_CHECK(hipDeviceSynchronize());
             }
             R.plan = make_halo_plan(R.topo, R.gv.si, Z + 2, xself_);
@@ -458,6 +466,8 @@ private:
             (void)hipFree(R.ty);
             (void)hipFree(R.tz);
             (void)hipFree(R.txy);
+            (void)hipFree(R.rtxy);
+            (void)hipFree(R.rtz);
             for (auto* p : R.sbuf) (void)hipFree(p);
             for (auto* p : R.rbuf) (void)hipFree(p);
             (void)hipFree(R.err);
@@ -807,7 +817,7 @@ private:
         launch_tb2<T>(own ? tb_rows_ : 2, own ? tb_waves_ : 8, own ? tb_occ_ : 0, own ? tb_nwk_ : 1, cfg_.delta,
                       cfg_.fma && tb2_fma_supported(own ? tb_rows_ : 2, own ? tb_waves_ : 8, own ? tb_nwk_ : 1, cfg_.delta),
                       m == 1, A, B, R.g[lvl(m)], R.g[lvl(m + 1)], R.gv, boxes, nbox,
-                      R.cdom, R.error.i0, R.error.i1, R.wrap, R.wrap2, al, R.txy, R.tz,
+                      R.cdom, R.error.i0, R.error.i1, R.wrap, R.wrap2, al, R.txy, R.tz, R.rtxy, R.rtz,
                       coefs(m), coefs(m + 1), R.err + size_t(m) * kSlotsPerLayer,
                       R.err + size_t(m + 1) * kSlotsPerLayer, cfg_.chunk, s);
     }
@@ -858,7 +868,7 @@ private:
         const SeamPartners<T> sp = seam_partners(R, m, nullptr);
         if (!boxes) boxes = &R.compute, nbox = 1;
         launch_tb3<T>(tb_rows_, tb_waves_, cfg_.delta, cfg_.fma, m == 1, A, B, R.g[lvl(m + 1)], R.g[lvl(m + 2)], R.gv, boxes,
-                      nbox, R.cdom, R.error.i0, R.error.i1, R.wrap2, R.wrap3, sp, R.txy, R.tz,
+                      nbox, R.cdom, R.error.i0, R.error.i1, R.wrap2, R.wrap3, sp, R.txy, R.tz, R.rtxy, R.rtz,
                       coefs(m), coefs(m + 1), coefs(m + 2), R.err + size_t(m) * kSlotsPerLayer,
                       R.err + size_t(m + 1) * kSlotsPerLayer, R.err + size_t(m + 2) * kSlotsPerLayer,
                       cfg_.chunk, s);

@@ -24,6 +24,7 @@
 #include <algorithm>
 #include <cstdlib>
 #include <climits>
+#include <cmath>
 #include <type_traits>
 
 #include "device_common.hpp"
@@ -63,6 +64,9 @@ struct TbParams {
     const T* txy;
     int tpj;
     const T* tz;
+    const T* rtxy;  // --math fma: 1/|txy|, 1/|tz| (launch_recip_abs) for the relative error
+    const T* rtz;
+    T ict[2];       // --math fma: 1/|ct| of layers C, D
     T hx2, hy2, hz2, coefC, coefD, ctC, ctD;
     T yx2, yy2, yz2;  // RN(1/h^2): correctly rounded constant division
     T fc[2][3];       // --math fma: coef/h^2 of layers C, D per axis
@@ -166,9 +170,11 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WP
         os[r] = boff(j, k, ovalid[r]);
     }
     const T otz = (k >= Bx.k0 && k <= Bx.k1) ? p.tz[k] : T(0);
+    const T ortz = FM && k >= Bx.k0 && k <= Bx.k1 ? p.rtz[k] : T(0);
     // rows of this wave in the sx*sy table (launch_txy pads past the last row, so rows beyond
     // the box — never used, their lanes are masked — are in-bounds reads)
     const T* const txw = p.txy + jrow;
+    const T* const rtw = FM ? p.rtxy + jrow : nullptr;
 
     // Rare per-plane events of this work item as wave-uniform bits, so the common plane pays
     // one scalar test for all of them: C / D self-wrap ranges met (1, 2 / 4, 8), seam alias
@@ -251,7 +257,8 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WP
     }
 
     T ma1 = T(kErrInit), ma2 = T(kErrInit);
-    RelArg<T> mr1, mr2;
+    using Rel = std::conditional_t<FM, RelMax<T>, RelArg<T>>;  // fma: |d| * 1/|f| max
+    Rel mr1, mr2;
     T chk1 = T(0), chk2 = T(0);
 
     // layer L (0 = C, 1 = D) arithmetic: exact Laplacian or (FM) coef*Laplacian, and the updates
@@ -280,7 +287,7 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WP
 
     // errors and finiteness sum of one own plane i of a layer (values v[r]); the uniform plane
     // test outside the per-lane row masks keeps it a scalar branch
-    auto errors = [&](const T(&v)[R], const int i, const T ct, T& ma, RelArg<T>& mr, T& chk) {
+    auto errors = [&](const T(&v)[R], const int i, const T ct, T& ma, Rel& mr, T& chk) {
         if constexpr (ABL == 1) return;
         if (eplane(i)) {
             const T* const trow = txw + i * p.tpj;
@@ -292,6 +299,10 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WP
                 if constexpr (ABL == 2) {
                     const T e = absval(v[r] - f);
                     if (e > ma) ma = e;
+                } else if constexpr (FM) {
+                    const T dv = v[r] - f;
+                    ma = max_abs(ma, dv);
+                    mr.add(dv, ldconst(rtw + i * p.tpj, r) * ortz);
                 } else {
                     accumulate_error_dev(v[r], f, ma, mr);
                 }
@@ -468,9 +479,13 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WP
         plane(Ph<3>{}, i);
         if (++i > ie + 1) break;
     }
-    commit_errors<T, NW>(ma1, mr1.value(), chk1, p.errC);
+    auto rel = [&](const Rel& m, int L) {
+        if constexpr (FM) return m.value(p.ict[L]);
+        else return m.value();
+    };
+    commit_errors<T, NW>(ma1, rel(mr1, 0), chk1, p.errC);
     __syncthreads();
-    commit_errors<T, NW>(ma2, mr2.value(), chk2, p.errD);
+    commit_errors<T, NW>(ma2, rel(mr2, 1), chk2, p.errD);
 }
 
 }  // namespace
@@ -548,8 +563,9 @@ template <class T>
 void launch_tb2(int rows, int waves, int occ, int nwk, bool delta, bool fm, bool first, const T* A, const T* B, T* C, T* D, const GridView& gv,
                 const Box* boxes, int nbox, const Box& cdom, int ei0, int ei1, const Wrap& wrapC,
                 const Wrap& wrapD, const SeamAlias<T>& alias, const T* txy, const T* tz,
-                const StepCoefs& cC, const StepCoefs& cD, u64* errC, u64* errD,
+                const T* rtxy, const T* rtz, const StepCoefs& cC, const StepCoefs& cD, u64* errC, u64* errD,
                 int chunk, hipStream_t s) {
+    W3D_REQUIRE(!fm || (rtxy && rtz), "tb2 --math fma needs the reciprocal analytic tables");
     W3D_REQUIRE(gv.G >= 2, "temporal blocking needs ghost depth >= 2");
     W3D_REQUIRE(tb2_supported(rows, waves, occ, nwk), "tb2: unsupported rows x waves x occupancy x k-waves");
     W3D_REQUIRE(!delta || (occ == 0 && tb2_delta_supported(rows, waves, nwk)),
@@ -593,6 +609,8 @@ void launch_tb2(int rows, int waves, int occ, int nwk, bool delta, bool fm, bool
     p.txy = txy;
     p.tpj = gv.Y + 2;
     p.tz = tz;
+    p.rtxy = rtxy, p.rtz = rtz;
+    p.ict[0] = T(1 / std::fabs(cC.ct)), p.ict[1] = T(1 / std::fabs(cD.ct));
     p.hx2 = T(cC.hx2);
     p.hy2 = T(cC.hy2);
     p.hz2 = T(cC.hz2);
@@ -651,7 +669,7 @@ void launch_tb2(int rows, int waves, int occ, int nwk, bool delta, bool fm, bool
     template void launch_tb2<T>(int, int, int, int, bool, bool, bool, const T*, const T*, T*, T*, const GridView&, \
                                 const Box*, int, const Box&, int, int, const Wrap&,          \
                                 const Wrap&, const SeamAlias<T>&, const T*, const T*,        \
-                                const StepCoefs&, const StepCoefs&, u64*, u64*,              \
+                                const T*, const T*, const StepCoefs&, const StepCoefs&, u64*, u64*, \
                                 int, hipStream_t);
 W3D_TB_INST(double)
 W3D_TB_INST(float)

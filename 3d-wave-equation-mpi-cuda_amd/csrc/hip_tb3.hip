@@ -26,6 +26,7 @@
 
 #include <algorithm>
 #include <climits>
+#include <cmath>
 #include <type_traits>
 
 #include "device_common.hpp"
@@ -61,9 +62,12 @@ struct Tb3Params {
     const T* txy;
     int tpj;
     const T* tz;
+    const T* rtxy;  // --math fma: 1/|txy|, 1/|tz| (launch_recip_abs) for the relative error
+    const T* rtz;
     T hx2, hy2, hz2, yx2, yy2, yz2;
     T coefC, coefD, coefE, ctC, ctD, ctE;
     T fc[3][3];  // --math fma: coef/h^2 per layer (C, D, E) and axis
+    T ict[3];    // --math fma: 1/|ct| per layer
     u64* errC;
     u64* errD;
     u64* errE;
@@ -155,8 +159,10 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WP
         os[r] = boff(j, k, ovalid[r]);
     }
     const T otz = (k >= Bx.k0 && k <= Bx.k1) ? p.tz[k] : T(0);
+    const T ortz = FM && k >= Bx.k0 && k <= Bx.k1 ? p.rtz[k] : T(0);
     // rows of this wave in the sx*sy table (padded past the last row: masked rows read in bounds)
     const T* const txw = p.txy + (jt + w * R);
+    const T* const rtw = FM ? p.rtxy + (jt + w * R) : nullptr;
     // self-wrap ranges of D / E met by this work item (wave-uniform bits, one test per plane)
     int rare = 0;
 #pragma unroll
@@ -232,9 +238,10 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WP
     }
 
     T ma1 = T(kErrInit), ma2 = T(kErrInit);
-    RelArg<T> mr1, mr2;
+    using Rel = std::conditional_t<FM, RelMax<T>, RelArg<T>>;  // fma: |d| * 1/|f| max
+    Rel mr1, mr2;
     T ma3 = T(kErrInit);
-    RelArg<T> mr3;
+    Rel mr3;
     T chk1 = T(0), chk2 = T(0), chk3 = T(0);
 
     // Layer L (0 = C, 1 = D, 2 = E) arithmetic. lap(): the Laplacian (exact) or coef*Laplacian
@@ -267,7 +274,7 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WP
     };
     // errors and finiteness sum of the own nodes of plane i of a layer (values v[r]); the
     // uniform error-plane test sits outside the per-lane row masks (a scalar branch)
-    auto errors = [&](const T(&v)[R], const int i, const T ct, T& ma, RelArg<T>& mr, T& chk) {
+    auto errors = [&](const T(&v)[R], const int i, const T ct, T& ma, Rel& mr, T& chk) {
         if (i >= p.ei0 && i <= p.ei1) {
             const T* const trow = txw + i * p.tpj;
 #pragma unroll
@@ -275,7 +282,13 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WP
                 if (!ovalid[r]) continue;
                 chk += v[r];
                 const T f = (ldconst(trow, r) * otz) * ct;  // = ((sx*sy)*sz)*ct, stencil_math analytic
-                accumulate_error_dev(v[r], f, ma, mr);
+                if constexpr (FM) {
+                    const T dv = v[r] - f;
+                    ma = max_abs(ma, dv);
+                    mr.add(dv, ldconst(rtw + i * p.tpj, r) * ortz);
+                } else {
+                    accumulate_error_dev(v[r], f, ma, mr);
+                }
             }
         } else {
 #pragma unroll
@@ -517,11 +530,15 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WP
         step(Ph<3>{}, i);
         if (++i > ie + 2) break;
     }
-    commit_errors<T, NW>(ma1, mr1.value(), chk1, p.errC);
+    auto rel = [&](const Rel& m, int L) {
+        if constexpr (FM) return m.value(p.ict[L]);
+        else return m.value();
+    };
+    commit_errors<T, NW>(ma1, rel(mr1, 0), chk1, p.errC);
     __syncthreads();
-    commit_errors<T, NW>(ma2, mr2.value(), chk2, p.errD);
+    commit_errors<T, NW>(ma2, rel(mr2, 1), chk2, p.errD);
     __syncthreads();
-    commit_errors<T, NW>(ma3, mr3.value(), chk3, p.errE);
+    commit_errors<T, NW>(ma3, rel(mr3, 2), chk3, p.errE);
 }
 
 // C (layer m) on one partner plane of the periodic seam, every (j, k) of the storage except
@@ -621,8 +638,9 @@ template <class T>
 void launch_tb3(int rows, int waves, bool delta, bool fm, bool first, const T* A, const T* B, T* D, T* E,
                 const GridView& gv, const Box* boxes, int nbox, const Box& cdom, int ei0, int ei1,
                 const Wrap& wrapD, const Wrap& wrapE, const SeamPartners<T>& seam, const T* txy,
-                const T* tz, const StepCoefs& cC, const StepCoefs& cD,
+                const T* tz, const T* rtxy, const T* rtz, const StepCoefs& cC, const StepCoefs& cD,
                 const StepCoefs& cE, u64* errC, u64* errD, u64* errE, int chunk, hipStream_t s) {
+    W3D_REQUIRE(!fm || (rtxy && rtz), "tb3 --math fma needs the reciprocal analytic tables");
     W3D_REQUIRE(gv.G >= 3, "three-layer temporal blocking needs ghost depth >= 3");
     W3D_REQUIRE(tb3_supported(rows, waves, fm && !delta), "tb3: unsupported rows x waves (x --math fma)");
     W3D_REQUIRE(!delta || tb3_delta_supported(rows, waves, fm), "tb3 increment form: tiles r2w8, r1w8 only");
@@ -655,6 +673,8 @@ void launch_tb3(int rows, int waves, bool delta, bool fm, bool first, const T* A
     p.coefC = T(cC.coef), p.coefD = T(cD.coef), p.coefE = T(cE.coef);
     p.ctC = T(cC.ct), p.ctD = T(cD.ct), p.ctE = T(cE.ct);
     fma_coefs(cC, p.fc[0]), fma_coefs(cD, p.fc[1]), fma_coefs(cE, p.fc[2]);
+    p.rtxy = rtxy, p.rtz = rtz;
+    p.ict[0] = T(1 / std::fabs(cC.ct)), p.ict[1] = T(1 / std::fabs(cD.ct)), p.ict[2] = T(1 / std::fabs(cE.ct));
     p.errC = errC, p.errD = errD, p.errE = errE;
     const int TJ = waves * rows;
     int nb = 0, total = 0;
@@ -720,7 +740,7 @@ template void launch_seam_c<float>(bool, bool, bool, const SeamCPlane<float>*, i
     template void launch_tb3<T>(int, int, bool, bool, bool, const T*, const T*, T*, T*, const GridView&, \
                                 const Box*, int, const Box&, int, int, const Wrap&,           \
                                 const Wrap&, const SeamPartners<T>&, const T*,                \
-                                const T*, const StepCoefs&, const StepCoefs&,                 \
+                                const T*, const T*, const T*, const StepCoefs&, const StepCoefs&, \
                                 const StepCoefs&, u64*, u64*, u64*, int, hipStream_t);
 W3D_TB3_INST(double)
 W3D_TB3_INST(float)
