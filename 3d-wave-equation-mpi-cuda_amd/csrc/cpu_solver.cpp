@@ -122,6 +122,7 @@ public:
         res.transport = ext_ ? ext_->name() : (world_ > 1 ? "loopback" : "self");
         res.comm_size = ext_ ? ext_->comm_size() : 0;
         res.scheme = cfg_.delta ? "delta" : "leapfrog";
+        res.math = cfg_.fma ? "fma" : "exact";
         res.courant = prob_.courant;
         for (int a = 0; a < 3; ++a) res.dims[a] = ranks_[0].topo.dims[a];
         Timings t;
@@ -237,6 +238,10 @@ private:
         const T hx2 = T(prob_.hx2), hy2 = T(prob_.hy2), hz2 = T(prob_.hz2);
         const T coef = T(prob_.coef), coef1 = T(prob_.coef_first);
         const T cn = T(ct_[n]);
+        // --math fma: coef/h^2 folded (stencil_math coef_lap_fma), as the HIP kernels
+        const double cf = n == 1 ? prob_.coef_first : prob_.coef;
+        const T fx = T(cf / prob_.hx2), fy = T(cf / prob_.hy2), fz = T(cf / prob_.hz2);
+        const bool fm = cfg_.fma;
         const i64 si = R.si, sj = R.sj;
         const bool first = n == 1;
         double mabs = kErrInit, mrel = kErrInit;
@@ -253,15 +258,27 @@ private:
                     for (int k = cb.k0; k <= cb.k1; ++k) {
                         const i64 p = base + k;
                         const T c = u1[p];
-                        T lap = laplace7(c, u1[p - si], u1[p + si], u1[p - sj], u1[p + sj],
-                                         u1[p - 1], u1[p + 1], hx2, hy2, hz2);
                         T v;
-                        if (dnext) {
-                            const T d = first ? coef1 * lap : delta_incr(u[p], lap, coef);
-                            v = c + d;
-                            dnext[p] = d;
+                        if (fm) {
+                            const T l = coef_lap_fma(c, u1[p - si], u1[p + si], u1[p - sj], u1[p + sj], u1[p - 1],
+                                                     u1[p + 1], fx, fy, fz);
+                            if (dnext) {
+                                const T d = first ? l : u[p] + l;
+                                v = c + d;
+                                dnext[p] = d;
+                            } else {
+                                v = first ? c + l : leapfrog_fma(c, u2[p], l);
+                            }
                         } else {
-                            v = first ? taylor_first(c, lap, coef1) : leapfrog(c, u2[p], lap, coef);
+                            T lap = laplace7(c, u1[p - si], u1[p + si], u1[p - sj], u1[p + sj],
+                                             u1[p - 1], u1[p + 1], hx2, hy2, hz2);
+                            if (dnext) {
+                                const T d = first ? coef1 * lap : delta_incr(u[p], lap, coef);
+                                v = c + d;
+                                dnext[p] = d;
+                            } else {
+                                v = first ? taylor_first(c, lap, coef1) : leapfrog(c, u2[p], lap, coef);
+                            }
                         }
                         u[p] = v;
                         lb |= nonfinite(v);

@@ -59,9 +59,24 @@ struct StepParams {
     const T* tz;
     T hx2, hy2, hz2, coef, ct;
     T rx2, ry2, rz2;  // 1/h^2 (fast-math variants only)
+    int fm;           // --math fma (k_naive / k_flat; k_march: the FAST instantiation)
+    T fc[3];          // --math fma: coef/h^2 per axis
     T yx2, yy2, yz2;  // RN(1/h^2) in T for the correctly rounded constant division
     u64* err;
 };
+
+// One node of the one-point-per-lane kernels: exact (the reference's operation order) or the
+// --math fma form; leapfrog, Taylor start, or increment form (u2 holds d^{n-1})
+template <class T, bool FIRST>
+__device__ __forceinline__ T point_update(const StepParams<T>& p, T c, T xm, T xp, T ym, T yp, T zm, T zp, i64 o) {
+    if (p.fm) {
+        const T l = coef_lap_fma(c, xm, xp, ym, yp, zm, zp, p.fc[0], p.fc[1], p.fc[2]);
+        return FIRST ? c + l : (p.delta ? c + (p.u2[o] + l) : leapfrog_fma(c, p.u2[o], l));
+    }
+    const T lap = laplace7_cr(c, xm, xp, ym, yp, zm, zp, p.hx2, p.hy2, p.hz2, p.yx2, p.yy2, p.yz2);
+    return FIRST ? taylor_first(c, lap, p.coef)
+                 : (p.delta ? c + delta_incr(p.u2[o], lap, p.coef) : leapfrog(c, p.u2[o], lap, p.coef));
+}
 
 template <class T>
 __device__ __forceinline__ void store_point(const StepParams<T>& p, int i, int j, int k, i64 o,
@@ -231,12 +246,10 @@ __global__ void __launch_bounds__(kThreads) k_march(const StepParams<T> p) {
                 km = V{lds[H0][lr][lane], lds[H0][lr + 1][lane]};
                 kp = V{lds[H0][lr][lane + 2], lds[H0][lr + 1][lane + 2]};
             }
-            if constexpr (FAST) {
-                const V lap = laplace7_fast(c, u1[S0][v], u1[S2][v], jm, jp, km, kp,
-                                            vsplat<L, V>(p.rx2), vsplat<L, V>(p.ry2),
-                                            vsplat<L, V>(p.rz2));
-                vv[v] = FIRST ? __builtin_fma(p.coef, lap, c)
-                              : __builtin_fma(p.coef, lap, T(2) * c - u2[H0][v]);
+            if constexpr (FAST) {  // --math fma (stencil_math coef_lap_fma)
+                const V l = coef_lap_fma(c, u1[S0][v], u1[S2][v], jm, jp, km, kp, vsplat<L, V>(p.fc[0]),
+                                         vsplat<L, V>(p.fc[1]), vsplat<L, V>(p.fc[2]));
+                vv[v] = FIRST ? c + l : leapfrog_fma(c, u2[H0][v], l);
             } else {
                 const V lap = laplace7_cr(c, u1[S0][v], u1[S2][v], jm, jp, km, kp, hx2, hy2, hz2,
                                           yx2, yy2, yz2);
@@ -319,11 +332,8 @@ __global__ void __launch_bounds__(kThreads) k_naive(const StepParams<T> p) {
         for (int i = ib; i <= ie; ++i) {
             const i64 o = i64(i) * si + rowoff;
             const T c = p.u1[o];
-            const T lap = laplace7_cr(c, p.u1[o - si], p.u1[o + si], p.u1[o - p.sj],
-                                      p.u1[o + p.sj], p.u1[o - 1], p.u1[o + 1], p.hx2, p.hy2,
-                                      p.hz2, p.yx2, p.yy2, p.yz2);
-            const T v = FIRST ? taylor_first(c, lap, p.coef)
-                        : (p.delta ? c + delta_incr(p.u2[o], lap, p.coef) : leapfrog(c, p.u2[o], lap, p.coef));
+            const T v = point_update<T, FIRST>(p, c, p.u1[o - si], p.u1[o + si], p.u1[o - p.sj], p.u1[o + p.sj],
+                                               p.u1[o - 1], p.u1[o + 1], o);
             store_point(p, i, j, k, o, rowoff, v);
             chk += v;
             if (i >= p.ei0 && i <= p.ei1)
@@ -357,11 +367,8 @@ __global__ void __launch_bounds__(kThreads) k_flat(const StepParams<T> p) {
         const int rowoff = j * p.sj + k;
         const i64 o = i64(i) * si + rowoff;
         const T c = p.u1[o];
-        const T lap = laplace7_cr(c, p.u1[o - si], p.u1[o + si], p.u1[o - p.sj], p.u1[o + p.sj],
-                                  p.u1[o - 1], p.u1[o + 1], p.hx2, p.hy2, p.hz2, p.yx2, p.yy2,
-                                  p.yz2);
-        const T v = FIRST ? taylor_first(c, lap, p.coef)
-                    : (p.delta ? c + delta_incr(p.u2[o], lap, p.coef) : leapfrog(c, p.u2[o], lap, p.coef));
+        const T v = point_update<T, FIRST>(p, c, p.u1[o - si], p.u1[o + si], p.u1[o - p.sj], p.u1[o + p.sj],
+                                           p.u1[o - 1], p.u1[o + 1], o);
         store_point(p, i, j, k, o, rowoff, v);
         chk += v;
         if (i >= p.ei0 && i <= p.ei1) accumulate_error_dev(v, analytic(p.tx[i], p.ty[j], p.tz[k], p.ct), ma, mr);
@@ -502,7 +509,7 @@ bool xcd_swizzle_enabled() {
 
 KernelVariant parse_kernel_variant(const std::string& name) {
     // naive | auto | march[R][nt|f|p], R in {2,4,8} (default 4); nt = non-temporal u^{n-2},
-    // f = fast-math ablation, p = packed fp32 pairs of rows (fp32 runs only)
+    // f = the --math fma form, p = packed fp32 pairs of rows (fp32 runs only)
     KernelVariant v;
     if (name == "naive") {
         v.march = false;
@@ -601,6 +608,8 @@ void launch_step(const KernelVariant& kind, bool first, const T* u1, const T* u2
     p.yx2 = T(1) / T(c.hx2);
     p.yy2 = T(1) / T(c.hy2);
     p.yz2 = T(1) / T(c.hz2);
+    p.fm = kind.fast ? 1 : 0;
+    p.fc[0] = T(c.coef / c.hx2), p.fc[1] = T(c.coef / c.hy2), p.fc[2] = T(c.coef / c.hz2);
     p.err = err;
     const bool march = kind.march && !kind.flat;
     const int tj_rows = march ? kWaves * kind.rows : kNaiveTJ;

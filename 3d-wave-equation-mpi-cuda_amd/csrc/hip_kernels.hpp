@@ -60,7 +60,7 @@ struct KernelVariant {
     bool march = true;
     int rows = 4;
     bool nt = false;
-    bool fast = false;  // reciprocal/FMA math: not bitwise-reproducible (benchmark ablation)
+    bool fast = false;  // --math fma form (stencil_math coef_lap_fma): not bitwise with the reference
     bool pk = false;    // packed fp32: two rows per v_pk_* instruction (fp32 only)
     bool flat = false;  // one point per thread over the flattened boxes (thin overlap shells)
     bool delta = false; // increment form: u2 holds d^{n-1} (naive / flat kernels only)

@@ -135,11 +135,12 @@ public:
         G_ = lay.G;
         L_ = lay.L;
         for (int a = 0; a < 3; ++a) cfg_.dims[a] = lay.dims[a];
-        W3D_REQUIRE(!c.fma || (tb_ && (tbd_ == 3 ? (c.delta ? tb3_delta_supported(tb_rows_, tb_waves_, true)
-                                                            : tb3_supported(tb_rows_, tb_waves_, true))
-                                                 : tb_occ_ == 0 && tb2_fma_supported(tb_rows_, tb_waves_, tb_nwk_, c.delta))),
-                    "--math fma needs a temporal-blocking kernel with an fma instantiation (tb3, tb3r1w8, "
-                    "tb3r1w16, tb2r2w8, tb2)");
+        W3D_REQUIRE(!c.fma || !tb_ ||
+                        (tbd_ == 3 ? (c.delta ? tb3_delta_supported(tb_rows_, tb_waves_, true)
+                                              : tb3_supported(tb_rows_, tb_waves_, true))
+                                   : tb_occ_ == 0 && tb2_fma_supported(tb_rows_, tb_waves_, tb_nwk_, c.delta)),
+                    "--math fma: no fma instantiation of this temporal-blocking tile (tb3, tb3r1w8, tb3r1w16, "
+                    "tb2r2w8, tb2)");
         W3D_REQUIRE(!tb_ || (tbd_ == 3 ? tb3_supported(tb_rows_, tb_waves_)
                                         : tb2_supported(tb_rows_, tb_waves_, tb_occ_, tb_nwk_)),
                     "wave3d: unknown kernel variant " + c.kernel);
@@ -158,6 +159,13 @@ public:
             kind_.march = false;
             kind_.delta = true;
             naive_.delta = true;
+        }
+        if (c.fma) {
+            // every kernel of the run (single-step tails and shells too) uses the FMA form, so a
+            // node's value does not depend on which kernel computed it
+            W3D_REQUIRE(!kind_.pk, "--math fma: no packed-fp32 march variant");
+            kind_.fast = true;
+            naive_.fast = true;
         }
         // interior/shell split + comm stream whenever there is a remote halo to hide
         overlap_ = c.overlap && (ext_ != nullptr || world_ > 1);

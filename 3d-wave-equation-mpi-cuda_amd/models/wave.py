@@ -35,6 +35,7 @@ class WaveProblem:
     pi: str = "ref"
     ic: str = "ref"
     scheme: str = "leapfrog"  # "delta": increment form (u^n = u^{n-1} + d^n), fp32 accuracy
+    math: str = "exact"       # "fma": coef/h^2 folded into FMAs (temporal-blocking kernels)
 
     def _pi(self) -> float:
         return PI_REF if self.pi == "ref" else math.pi
@@ -66,7 +67,8 @@ class WaveProblem:
     def args(self, Np: int = 1, **opts) -> list[str]:
         a = [str(self.N), str(Np), _len_arg(self.Lx), _len_arg(self.Ly), _len_arg(self.Lz),
              repr(float(self.T)), str(self.timesteps),
-             "--dtype", self.dtype, "--pi", self.pi, "--ic", self.ic, "--scheme", self.scheme]
+             "--dtype", self.dtype, "--pi", self.pi, "--ic", self.ic, "--scheme", self.scheme,
+             "--math", self.math]
         for k, v in opts.items():
             if v is None or v is False:
                 continue

@@ -263,3 +263,23 @@ def test_field_dump_matches_torch_reference(C, cpu_prog, tmp_path):
     subprocess.run([cpu_prog] + p.args(1) + ["--ranks", "2", "--dump", path, "--format", "none",
                                               "--quiet"], check=True, cwd=tmp_path)
     assert np.array_equal(np.load(path), ref)
+
+
+@pytest.mark.parametrize("scheme,dtype", [("leapfrog", "fp64"), ("delta", "fp64"), ("leapfrog", "fp32"),
+                                          ("delta", "fp32")])
+def test_fma_math_oracle(C, scheme, dtype):
+    """--math fma on the OpenMP oracle (the HIP kernels' FMA form, node for node): L-inf abs
+    equal to the exact form's within rounding (fp64: 6 significant digits, as printed), the
+    same on any decomposition bit for bit."""
+    import wave3d
+
+    p = wave3d.WaveProblem(24, Lx=1.3, Ly="pi", Lz=2.0, timesteps=17, ic="shifted", scheme=scheme, dtype=dtype)
+    ex = _solve(p)
+    p.math = "fma"
+    fm = _solve(p)
+    assert fm.extra["math"] == "fma" and ex.extra["math"] == "exact"
+    if dtype == "fp64":
+        assert [f"{a:.6g}" for a in fm.max_abs] == [f"{a:.6g}" for a in ex.max_abs]
+    else:
+        assert fm.max_abs[-1] == pytest.approx(ex.max_abs[-1], rel=2e-2)
+    assert _solve(p, ranks=4).max_abs == fm.max_abs

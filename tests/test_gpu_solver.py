@@ -421,12 +421,17 @@ def test_fma_math_goldens(C, kernel):
     r = wave3d.WaveSolver(wave3d.WaveProblem(32, timesteps=20), "hip", kernel=kernel)
     r.opts["math"] = "fma"
     res = r.run()
-    assert res.extra["math"] == "fma" and _fmt(res) == GOLDEN_N32_K20
+    assert res.extra["math"] == "fma"
+    # L-inf abs: the reference's 6 digits on every layer. The max relative error is set by the
+    # nodes next to f's zero plane (sin(PI_ref) ~ 9e-11), where |u - f| is at the rounding noise
+    # of the stencil: any other rounding order moves it in the 3rd-4th digit
+    for (a, r_), (ga, gr) in zip(_fmt(res), GOLDEN_N32_K20):
+        assert a == ga and float(r_) == pytest.approx(float(gr), rel=1e-2)
     r = wave3d.WaveSolver(wave3d.WaveProblem(512, timesteps=100), "hip", kernel=kernel)
     r.opts["math"] = "fma"
     got = _fmt(r.run())
-    for layer, val in GOLDEN_SPOTS[(512, 100, "ref")].items():
-        assert got[layer] == val
+    for layer, (a, _) in GOLDEN_SPOTS[(512, 100, "ref")].items():
+        assert got[layer][0] == a
 
 
 @pytest.mark.parametrize("kernel", ["tb3", "tb2r2w8"])
@@ -444,3 +449,24 @@ def test_fma_math_decomposition_invariance(C, kernel, ranks, dims):
     many.opts["math"] = "fma"
     a, b = one.run(), many.run()
     assert a.max_abs == b.max_abs and a.max_rel == b.max_rel
+
+
+@pytest.mark.parametrize("kernel,scheme,dtype", [("auto", "leapfrog", "fp64"), ("tb3", "leapfrog", "fp64"),
+                                                 ("tb2r2w8", "leapfrog", "fp64"), ("march4", "leapfrog", "fp64"),
+                                                 ("naive", "leapfrog", "fp64"), ("auto", "delta", "fp32"),
+                                                 ("auto", "leapfrog", "fp32"), ("tb2r2w8", "delta", "fp64")])
+@pytest.mark.parametrize("ranks", [1, 8])
+def test_fma_math_matches_oracle(C, kernel, scheme, dtype, ranks):
+    """--math fma on every kernel family against the OpenMP oracle's FMA form: the values — and
+    so the per-layer max abs errors — bit for bit (same operations per node); the max relative
+    error within rounding of the reference's quotient (RelMax, device_common.hpp)."""
+    import wave3d
+
+    p = wave3d.WaveProblem(48, Lx=1.3, Ly="pi", Lz=2.0, timesteps=23, ic="shifted", scheme=scheme, dtype=dtype,
+                           math="fma")
+    g = _solve(p, kernel=kernel, ranks=ranks if ranks > 1 else 0, overlap=True)
+    c = _solve(p, backend="cpu", threads=8)
+    assert g.extra["math"] == "fma" and c.extra["math"] == "fma"
+    assert g.max_abs == c.max_abs
+    for a, b in zip(g.max_rel, c.max_rel):
+        assert a == pytest.approx(b, rel=1e-9 if dtype == "fp64" else 1e-4)
