@@ -12,7 +12,7 @@ for rep in $(seq ${ROUNDS:-2}); do
   for arm in $ARMS; do
     k=${arm%%:*}; m=${arm##*:}
     echo -n "round=$rep kernel=$k math=$m "
-    timeout -k 10 120 $B $N 1 pi pi pi 1 $K --dtype $DT --kernel $k --math $m --repeat 5 --warmup 1 --json --quiet \
+    timeout -k 10 120 $B $N 1 pi pi pi 1 $K --dtype $DT --scheme ${SCHEME:-leapfrog} --kernel $k --math $m --repeat 5 --warmup 1 --json --quiet \
         --format none | python3 -c "import sys,json; r=json.loads(sys.stdin.read().splitlines()[-1]); print(round(r['mpts_per_s_best']), '%.9g' % r['linf_abs'], r['kernel'], r['math'])" || exit 1
   done
 done
