@@ -58,7 +58,6 @@ struct StepParams {
     const T* ty;
     const T* tz;
     T hx2, hy2, hz2, coef, ct;
-    T rx2, ry2, rz2;  // 1/h^2 (fast-math variants only)
     int fm;           // --math fma (k_naive / k_flat; k_march: the FAST instantiation)
     T fc[3];          // --math fma: coef/h^2 per axis
     T yx2, yy2, yz2;  // RN(1/h^2) in T for the correctly rounded constant division
@@ -602,9 +601,6 @@ void launch_step(const KernelVariant& kind, bool first, const T* u1, const T* u2
     p.hz2 = T(c.hz2);
     p.coef = T(c.coef);
     p.ct = T(c.ct);
-    p.rx2 = T(1.0 / c.hx2);
-    p.ry2 = T(1.0 / c.hy2);
-    p.rz2 = T(1.0 / c.hz2);
     p.yx2 = T(1) / T(c.hx2);
     p.yy2 = T(1) / T(c.hy2);
     p.yz2 = T(1) / T(c.hz2);

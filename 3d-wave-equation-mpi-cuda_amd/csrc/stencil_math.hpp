@@ -122,34 +122,26 @@ W3D_HD T laplace7_cr(T c, T xm, T xp, T ym, T yp, T zm, T zp, T hx2, T hy2, T hz
     return ans;
 }
 
-// ---- fast-math variants (not bitwise-reproducible: reciprocal multiplies, FMAs) --------
-template <class T>
-W3D_HD T laplace7_fast(T c, T xm, T xp, T ym, T yp, T zm, T zp, T rx2, T ry2, T rz2) {
-    T two_c = T(2) * c;
-    T ans = (zm + zp - two_c) * rz2;
-    ans = __builtin_fma(ym + yp - two_c, ry2, ans);
-    return __builtin_fma(xm + xp - two_c, rx2, ans);
-}
-
-template <class T>
-W3D_HD void accumulate_error_fast(T u, T f, T& mabs, T& mrel) {
-    T ea = absval(u - f);
-    T er = ea / absval(f);
-    if (ea > mabs) mabs = ea;
-    if (er > mrel) mrel = er;
-}
-
 // ---- FMA form (--math fma): the same scheme with coef/h^2 folded into three constants ------
 // coef*lap = cx*((xm + xp) - 2c) + cy*(...) + cz*(...), cd = coef/hd^2: every second difference
 // is still formed before it is scaled (no loss of the small h^2 u'' term, so fp32 keeps its
 // accuracy), 8 FP operations instead of the exact form's ~19 (three correctly rounded
 // divisions), rounded differently from the reference CPU programs — as nvcc's default FMA
 // contraction rounds the reference's own CUDA kernel (cuda_sol_kernels.cu:36-38) differently.
+// fp64: s = fma(-2, c, xm + xp) (2 ops; its rounding, ~eps*|u|, is far below the scheme's
+// error). fp32, whose error the rounding sets: s = (xm - c) + (xp - c) — each difference of
+// neighbouring values is exact (Sterbenz), so s carries one rounding of a quantity of size h*u'
+// instead of one of size u: more accurate than the reference's (xm - 2c) + xp too.
+W3D_HD double second_diff(double m, double c, double p) { return fma_t(-2.0, c, m + p); }
+W3D_HD float second_diff(float m, float c, float p) { return (m - c) + (p - c); }
+#ifdef __HIPCC__
+__device__ __forceinline__ f32x2 second_diff(f32x2 m, f32x2 c, f32x2 p) { return (m - c) + (p - c); }
+#endif
 template <class T>
 W3D_HD T coef_lap_fma(T c, T xm, T xp, T ym, T yp, T zm, T zp, T cx, T cy, T cz) {
-    const T sx = fma_t(T(-2), c, xm + xp);
-    const T sy = fma_t(T(-2), c, ym + yp);
-    const T sz = fma_t(T(-2), c, zm + zp);
+    const T sx = second_diff(xm, c, xp);
+    const T sy = second_diff(ym, c, yp);
+    const T sz = second_diff(zm, c, zp);
     return fma_t(cx, sx, fma_t(cy, sy, cz * sz));
 }
 // leapfrog with a pre-scaled Laplacian l = coef*lap: (2c - u2) + l

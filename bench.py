@@ -58,6 +58,10 @@ def main() -> int:
                     help="time stepping: leapfrog (the reference's), delta (increment form, same scheme "
                          "without the 2u-u cancellation); auto = leapfrog for fp64, delta for fp32 "
                          "(profiles/fp32_scheme_r3.txt)")
+    ap.add_argument("--math", default="auto", choices=["auto", "exact", "fma"],
+                    help="stencil arithmetic: exact = the reference CPU programs' operation order, bit for "
+                         "bit; fma = coef/h^2 folded into fused multiply-adds (same scheme, same L-inf abs to "
+                         "9 digits at the headline config, profiles/math_fma_r3.txt); auto = fma on the GPU")
     ap.add_argument("--fp64-ref", default="auto", choices=["auto", "on", "off"],
                     help="fp32 runs: after timing, solve the same N/K/decomposition in fp64 and report "
                          "its L-inf as linf_fp64_ref (BASELINE.md §4 config 5); auto = on for fp32")
@@ -154,7 +158,9 @@ def main() -> int:
     a.timesteps = K
     if a.scheme == "auto":
         a.scheme = presets.default_scheme(a.dtype)
-    prob = wave3d.WaveProblem(N, timesteps=a.timesteps, dtype=a.dtype, scheme=a.scheme)
+    if a.math == "auto":
+        a.math = presets.default_math(a.backend, a.dtype)
+    prob = wave3d.WaveProblem(N, timesteps=a.timesteps, dtype=a.dtype, scheme=a.scheme, math=a.math)
     if not prob.stable():
         print(f"bench: warning: C={prob.courant:.3f} > 1/sqrt(3) (unstable)", file=sys.stderr)
     solver = wave3d.WaveSolver(prob, a.backend, transport=transport, Np=n_gpus, kernel=a.kernel, dims=dims,
@@ -202,6 +208,7 @@ def main() -> int:
         "vs_baseline": round(value / base, 3),
         "dtype": a.dtype,
         "scheme": res.get("scheme", a.scheme),
+        "math": res.get("math", a.math),
         "data": "synthetic (analytic initial condition u=sin(2pi x/Lx)sin(pi y/Ly)sin(pi z/Lz))",
         "config": {
             "model": f"wave3d {a.scheme} 7-point, N={N}^3, L=pi, T=1, timesteps={a.timesteps}",
@@ -246,7 +253,7 @@ def main() -> int:
     if a.dtype == "fp32" and a.fp64_ref != "off" or a.fp64_ref == "on":
         # the fp64 L-inf of the same N, K and decomposition (config 5 compares
         # against its own fp64 run), after the timed region and after the fp32 session is freed
-        p64 = wave3d.WaveProblem(N, timesteps=a.timesteps, dtype="fp64")
+        p64 = wave3d.WaveProblem(N, timesteps=a.timesteps, dtype="fp64", math=presets.default_math(a.backend, "fp64"))
         s64 = wave3d.WaveSolver(p64, a.backend, transport=transport, Np=n_gpus, kernel="auto", dims=dims,
                                 overlap="off" if a.no_overlap else a.overlap,
                                 device=(torch.cuda.current_device() if a.backend == "hip" else None))

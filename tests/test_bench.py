@@ -72,6 +72,7 @@ def test_bench_gpu_default_config_short():
     r = _bench(["--steps", "1", "--warmup", "1"])
     _check(r, 1, 1, 1)
     assert r["scaling"] == "weak" and r["config"]["N"] == 512 and r["config"]["timesteps"] == 100
+    assert r["math"] == "fma" and r["config"]["kernel"] == "tb3r1w8"  # the GPU default (presets)
     assert f"{r['linf_abs']:.6g}" == "6.03381e-07"  # golden N=512 K=100
     assert r["linf_golden"] == 6.03381e-07 and r["linf_ok"] is True
     assert r["config"]["dims"] == [1, 1, 1] and r["config"]["overlap"] is False  # no remote halo
@@ -117,7 +118,7 @@ def test_bench_gpu_fp32_two_ranks_staged(scheme, linf):
     L-inf of the single-GPU run (leapfrog 4.47035e-06, profiles/fp32_accuracy_r2.txt; the fp32
     default, the increment form, 1.3113e-06), and the fp64 L-inf of the same run (the golden)."""
     r = _bench(["--steps", "1", "--warmup", "0", "--dtype", "fp32", "--transport", "staged",
-                "--shared-device", "--overlap", "on", "--scheme", scheme], nproc=2, timeout=600)
+                "--shared-device", "--overlap", "on", "--scheme", scheme, "--math", "exact"], nproc=2, timeout=600)
     assert r["dtype"] == "fp32" and r["n_gpus"] == 2 and r["config"]["dims"] == [2, 1, 1]
     assert r["config"]["kernel"] == "tb3" and r["config"]["overlap"] is True
     assert r["scheme"] == ("delta" if scheme == "auto" else scheme)
