@@ -245,19 +245,19 @@ void k_tb3_dense(int rows, int waves, bool fm, bool first, uintptr_t A, uintptr_
     T* rt = nullptr;  // --math fma: 1/|txy| then 1/|tz|
     const size_t ntxy = txy_elems(v.X, v.Y), ntz = size_t(v.Z) + 2;
     if (hipMalloc(&txy, ntxy * sizeof(T)) != hipSuccess) throw Error("k_tb3: hipMalloc failed");
-    if (fm && hipMalloc(&rt, (ntxy + ntz) * sizeof(T)) != hipSuccess) {
+    if (fm && hipMalloc(&rt, (2 * ntxy + ntz) * sizeof(T)) != hipSuccess) {
         (void)hipFree(txy);
         throw Error("k_tb3: hipMalloc failed");
     }
     try {
         launch_txy<T>(txy, P<T>(tx), P<T>(ty), v.X, v.Y, s);
         if (fm) {
-            launch_recip_abs<T>(rt, txy, ntxy, s);
-            launch_recip_abs<T>(rt + ntxy, P<T>(tz), ntz, s);
+            launch_txr<T>(rt, txy, ntxy, s);
+            launch_recip_abs<T>(rt + 2 * ntxy, P<T>(tz), ntz, s);
         }
         launch_tb3<T>(rows, waves, false, fm, first, P<T>(A) + o, P<T>(B) + o, P<T>(D) + o, P<T>(E) + o, v,
                       bx.data(), int(bx.size()), tobox(cdom), ei0, ei1, Wrap{}, Wrap{},
-                      SeamPartners<T>{}, txy, P<T>(tz), rt, fm ? rt + ntxy : nullptr, tocoefs(cC), tocoefs(cD),
+                      SeamPartners<T>{}, txy, P<T>(tz), rt, fm ? rt + 2 * ntxy : nullptr, tocoefs(cC), tocoefs(cD),
                       tocoefs(cE), P<u64>(errC), P<u64>(errD), P<u64>(errE), chunk, s);
     } catch (...) {
         (void)hipStreamSynchronize(s);

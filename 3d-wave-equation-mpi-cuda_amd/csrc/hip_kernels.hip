@@ -743,6 +743,22 @@ void launch_recip_abs(T* out, const T* in, size_t n, hipStream_t s) {
     hipLaunchKernelGGL(k_recip_abs<T>, dim3(unsigned((n + 255) / 256)), dim3(256), 0, s, out, in, n);
     HIP_OK(hipGetLastError());
 }
+namespace {
+template <class T>
+__global__ void k_txr(T* out, const T* txy, size_t n) {
+    const size_t q = size_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (q < n) out[2 * q] = txy[q], out[2 * q + 1] = T(1) / absval(txy[q]);
+}
+}  // namespace
+
+template <class T>
+void launch_txr(T* out, const T* txy, size_t n, hipStream_t s) {
+    if (n == 0) return;
+    hipLaunchKernelGGL(k_txr<T>, dim3(unsigned((n + 255) / 256)), dim3(256), 0, s, out, txy, n);
+    HIP_OK(hipGetLastError());
+}
+template void launch_txr<double>(double*, const double*, size_t, hipStream_t);
+template void launch_txr<float>(float*, const float*, size_t, hipStream_t);
 template void launch_recip_abs<double>(double*, const double*, size_t, hipStream_t);
 template void launch_recip_abs<float>(float*, const float*, size_t, hipStream_t);
 

@@ -127,7 +127,7 @@ template <class T>
 void launch_tb3(int rows, int waves, bool delta, bool fm, bool first, const T* A, const T* B, T* D, T* E,
                 const GridView& gv, const Box* boxes, int nbox, const Box& cdom, int ei0, int ei1,
                 const Wrap& wrapD, const Wrap& wrapE, const SeamPartners<T>& seam, const T* txy,
-                const T* tz, const T* rtxy, const T* rtz, const StepCoefs& cC, const StepCoefs& cD,
+                const T* tz, const T* txr, const T* rtz, const StepCoefs& cC, const StepCoefs& cD,
                 const StepCoefs& cE, u64* errC, u64* errD, u64* errE, int chunk, hipStream_t s);
 
 // Box halo staging for the temporal-blocking exchange on y/z splits: copy the logical box
@@ -195,7 +195,7 @@ template <class T>
 void launch_tb2(int rows, int waves, int occ, int nwk, bool delta, bool fm, bool first, const T* A, const T* B, T* C, T* D, const GridView& gv,
                 const Box* boxes, int nbox, const Box& cdom, int ei0, int ei1, const Wrap& wrapC,
                 const Wrap& wrapD, const SeamAlias<T>& alias, const T* txy, const T* tz,
-                const T* rtxy, const T* rtz, const StepCoefs& cC, const StepCoefs& cD, u64* errC, u64* errD,
+                const T* txr, const T* rtz, const StepCoefs& cC, const StepCoefs& cD, u64* errC, u64* errD,
                 int chunk, hipStream_t s);
 
 // Analytic-product table of the temporal-blocking kernels: out[i*(Y+2) + j] = RN(tx[i]*ty[j])
@@ -209,5 +209,9 @@ void launch_txy(T* out, const T* tx, const T* ty, int X, int Y, hipStream_t s);
 // then / |ct| once per layer, instead of a division or an exact argmax per node)
 template <class T>
 void launch_recip_abs(T* out, const T* in, size_t n, hipStream_t s);
+// --math fma pair table: out[2q] = txy[q], out[2q+1] = 1/|txy[q]| for q < txy_elems(X, Y): one
+// scalar load of both per row in the sweeps
+template <class T>
+void launch_txr(T* out, const T* txy, size_t n, hipStream_t s);
 
 }  // namespace wave3d

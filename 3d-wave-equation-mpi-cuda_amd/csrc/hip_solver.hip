@@ -67,7 +67,7 @@ struct DevRank {
     size_t elems = 0;                                  // allocation per level
     T *tx = nullptr, *ty = nullptr, *tz = nullptr;
     T* txy = nullptr;  // sx*sy table of the temporal-blocking sweep (launch_txy)
-    T* rtxy = nullptr;  // --math fma: 1/|txy|, 1/|tz| (relative error without division)
+    T* rtxy = nullptr;  // --math fma: (txy, 1/|txy|) pairs and 1/|tz| (relative error without division)
     T* rtz = nullptr;
     HaloPlan plan;
     std::vector<T*> sbuf, rbuf;  // y/z messages only (x messages live in the grid)
@@ -358,9 +358,9 @@ private:
                 HIP_CHECK(hipMalloc(&R.txy, txy_elems(X, Y) * sizeof(T)));
                 launch_txy<T>(R.txy, R.tx, R.ty, X, Y, nullptr);
                 if (cfg_.fma) {
-                    HIP_CHECK(hipMalloc(&R.rtxy, txy_elems(X, Y) * sizeof(T)));
+                    HIP_CHECK(hipMalloc(&R.rtxy, 2 * txy_elems(X, Y) * sizeof(T)));
                     HIP_CHECK(hipMalloc(&R.rtz, size_t(Z + 2) * sizeof(T)));
-                    launch_recip_abs<T>(R.rtxy, R.txy, txy_elems(X, Y), nullptr);
+                    launch_txr<T>(R.rtxy, R.txy, txy_elems(X, Y), nullptr);
                     launch_recip_abs<T>(R.rtz, R.tz, size_t(Z + 2), nullptr);
                 }
                 HIP_CHECK(hipDeviceSynchronize());

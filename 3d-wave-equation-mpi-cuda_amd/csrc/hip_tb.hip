@@ -64,7 +64,7 @@ struct TbParams {
     const T* txy;
     int tpj;
     const T* tz;
-    const T* rtxy;  // --math fma: 1/|txy|, 1/|tz| (launch_recip_abs) for the relative error
+    const T* txr;   // --math fma: (sx sy, 1/|sx sy|) pairs (launch_txr) and 1/|tz|
     const T* rtz;
     T ict[2];       // --math fma: 1/|ct| of layers C, D
     T hx2, hy2, hz2, coefC, coefD, ctC, ctD;
@@ -174,7 +174,9 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WP
     // rows of this wave in the sx*sy table (launch_txy pads past the last row, so rows beyond
     // the box — never used, their lanes are masked — are in-bounds reads)
     const T* const txw = p.txy + jrow;
-    const T* const rtw = FM ? p.rtxy + jrow : nullptr;
+    T om[R];  // --math fma: 1 on valid own nodes, 0 on masked lanes (branch-free errors)
+#pragma unroll
+    for (int r = 0; r < R; ++r) om[r] = ovalid[r] ? T(1) : T(0);
 
     // Rare per-plane events of this work item as wave-uniform bits, so the common plane pays
     // one scalar test for all of them: C / D self-wrap ranges met (1, 2 / 4, 8), seam alias
@@ -263,8 +265,10 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WP
 
     // layer L (0 = C, 1 = D) arithmetic: exact Laplacian or (FM) coef*Laplacian, and the updates
     auto lap = [&](int L, T ctr, T xm, T xp, T ym, T yp, T zm, T zp) {
-        if constexpr (FM)
-            return coef_lap_fma(ctr, xm, xp, ym, yp, zm, zp, p.fc[L][0], p.fc[L][1], p.fc[L][2]);
+        if constexpr (FM) {  // fc[0] == fc[1] unless C is the Taylor first layer
+            const int f = FIRST && L == 0 ? 0 : 1;
+            return coef_lap_fma(ctr, xm, xp, ym, yp, zm, zp, p.fc[f][0], p.fc[f][1], p.fc[f][2]);
+        }
         else
             return laplace7_cr(ctr, xm, xp, ym, yp, zm, zp, p.hx2, p.hy2, p.hz2, p.yx2, p.yy2, p.yz2);
     };
@@ -287,7 +291,7 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WP
 
     // errors and finiteness sum of one own plane i of a layer (values v[r]); the uniform plane
     // test outside the per-lane row masks keeps it a scalar branch
-    auto errors = [&](const T(&v)[R], const int i, const T ct, T& ma, Rel& mr, T& chk) {
+    auto errors_exact = [&](const T(&v)[R], const int i, const T ct, T& ma, auto& mr, T& chk) {
         if constexpr (ABL == 1) return;
         if (eplane(i)) {
             const T* const trow = txw + i * p.tpj;
@@ -299,10 +303,6 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WP
                 if constexpr (ABL == 2) {
                     const T e = absval(v[r] - f);
                     if (e > ma) ma = e;
-                } else if constexpr (FM) {
-                    const T dv = v[r] - f;
-                    ma = max_abs(ma, dv);
-                    mr.add(dv, ldconst(rtw + i * p.tpj, r) * ortz);
                 } else {
                     accumulate_error_dev(v[r], f, ma, mr);
                 }
@@ -314,6 +314,25 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WP
         }
     };
 
+    // --math fma: branch-free — every own plane, masked lanes and planes outside the error range
+    // contribute d = 0 (the multiplier om * em), so no exec-mask branches and no phi copies of the
+    // running maxima; one scalar load of the (sx sy, 1/|sx sy|) pair per row (txr table)
+    auto errors_fm = [&](const T(&v)[R], const int i, const T ct, T& ma, RelMax<T>& mr, T& chk) {
+        const T em = (i >= p.ei0 && i <= p.ei1) ? T(1) : T(0);
+        const T* const tr = p.txr + 2 * (i * p.tpj + jrow);
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            chk += ovalid[r] ? v[r] : T(0);
+            const T f = (ldconst(tr, 2 * r) * otz) * ct;  // = ((sx*sy)*sz)*ct
+            const T dv = (v[r] - f) * (om[r] * em);
+            ma = max_abs(ma, dv);
+            mr.add(dv, ldconst(tr, 2 * r + 1) * ortz);
+        }
+    };
+    auto errors = [&](const T(&v)[R], const int i, const T ct, T& ma, Rel& mr, T& chk) {
+        if constexpr (FM) errors_fm(v, i, ct, ma, mr, chk);
+        else errors_exact(v, i, ct, ma, mr, chk);
+    };
     // prefetch A(i+2) (own, both rings), B(i+1); on the last plane the
     // descriptors get 0 records, so the loads return 0 without touching memory (uniform,
     // no per-lane masking)
@@ -563,9 +582,9 @@ template <class T>
 void launch_tb2(int rows, int waves, int occ, int nwk, bool delta, bool fm, bool first, const T* A, const T* B, T* C, T* D, const GridView& gv,
                 const Box* boxes, int nbox, const Box& cdom, int ei0, int ei1, const Wrap& wrapC,
                 const Wrap& wrapD, const SeamAlias<T>& alias, const T* txy, const T* tz,
-                const T* rtxy, const T* rtz, const StepCoefs& cC, const StepCoefs& cD, u64* errC, u64* errD,
+                const T* txr, const T* rtz, const StepCoefs& cC, const StepCoefs& cD, u64* errC, u64* errD,
                 int chunk, hipStream_t s) {
-    W3D_REQUIRE(!fm || (rtxy && rtz), "tb2 --math fma needs the reciprocal analytic tables");
+    W3D_REQUIRE(!fm || (txr && rtz), "tb2 --math fma needs the reciprocal analytic tables");
     W3D_REQUIRE(gv.G >= 2, "temporal blocking needs ghost depth >= 2");
     W3D_REQUIRE(tb2_supported(rows, waves, occ, nwk), "tb2: unsupported rows x waves x occupancy x k-waves");
     W3D_REQUIRE(!delta || (occ == 0 && tb2_delta_supported(rows, waves, nwk)),
@@ -609,7 +628,7 @@ void launch_tb2(int rows, int waves, int occ, int nwk, bool delta, bool fm, bool
     p.txy = txy;
     p.tpj = gv.Y + 2;
     p.tz = tz;
-    p.rtxy = rtxy, p.rtz = rtz;
+    p.txr = txr, p.rtz = rtz;
     p.ict[0] = T(1 / std::fabs(cC.ct)), p.ict[1] = T(1 / std::fabs(cD.ct));
     p.hx2 = T(cC.hx2);
     p.hy2 = T(cC.hy2);

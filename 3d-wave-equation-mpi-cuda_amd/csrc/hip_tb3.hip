@@ -62,11 +62,13 @@ struct Tb3Params {
     const T* txy;
     int tpj;
     const T* tz;
-    const T* rtxy;  // --math fma: 1/|txy|, 1/|tz| (launch_recip_abs) for the relative error
+    const T* txr;   // --math fma: (sx sy, 1/|sx sy|) pairs (launch_txr) and 1/|tz|
     const T* rtz;
     T hx2, hy2, hz2, yx2, yy2, yz2;
     T coefC, coefD, coefE, ctC, ctD, ctE;
-    T fc[3][3];  // --math fma: coef/h^2 per layer (C, D, E) and axis
+    T fc[2][3];  // --math fma: coef/h^2 per axis of layer C (fc[0]) and of layers D, E (fc[1]);
+                 // equal unless C is the Taylor first layer (FIRST), so the non-FIRST sweep
+                 // keeps one triple in SGPRs
     T ict[3];    // --math fma: 1/|ct| per layer
     u64* errC;
     u64* errD;
@@ -162,7 +164,9 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WP
     const T ortz = FM && k >= Bx.k0 && k <= Bx.k1 ? p.rtz[k] : T(0);
     // rows of this wave in the sx*sy table (padded past the last row: masked rows read in bounds)
     const T* const txw = p.txy + (jt + w * R);
-    const T* const rtw = FM ? p.rtxy + (jt + w * R) : nullptr;
+    T om[R];  // --math fma: 1 on valid own nodes, 0 on masked lanes (branch-free errors)
+#pragma unroll
+    for (int r = 0; r < R; ++r) om[r] = ovalid[r] ? T(1) : T(0);
     // self-wrap ranges of D / E met by this work item (wave-uniform bits, one test per plane)
     int rare = 0;
 #pragma unroll
@@ -247,10 +251,12 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WP
     // Layer L (0 = C, 1 = D, 2 = E) arithmetic. lap(): the Laplacian (exact) or coef*Laplacian
     // (FM); leap / first / incr: the leapfrog, Taylor-start and increment updates from it.
     auto lap = [&](int L, T ctr, T xm, T xp, T ym, T yp, T zm, T zp) {
-        if constexpr (FM)
-            return coef_lap_fma(ctr, xm, xp, ym, yp, zm, zp, p.fc[L][0], p.fc[L][1], p.fc[L][2]);
-        else
+        if constexpr (FM) {
+            const int f = FIRST && L == 0 ? 0 : 1;
+            return coef_lap_fma(ctr, xm, xp, ym, yp, zm, zp, p.fc[f][0], p.fc[f][1], p.fc[f][2]);
+        } else {
             return laplace7_cr(ctr, xm, xp, ym, yp, zm, zp, p.hx2, p.hy2, p.hz2, p.yx2, p.yy2, p.yz2);
+        }
     };
     auto coefL = [&](int L) { return L == 0 ? p.coefC : (L == 1 ? p.coefD : p.coefE); };
     auto leap = [&](int L, T ctr, T u2, T l) {
@@ -274,7 +280,7 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WP
     };
     // errors and finiteness sum of the own nodes of plane i of a layer (values v[r]); the
     // uniform error-plane test sits outside the per-lane row masks (a scalar branch)
-    auto errors = [&](const T(&v)[R], const int i, const T ct, T& ma, Rel& mr, T& chk) {
+    auto errors_exact = [&](const T(&v)[R], const int i, const T ct, T& ma, auto& mr, T& chk) {
         if (i >= p.ei0 && i <= p.ei1) {
             const T* const trow = txw + i * p.tpj;
 #pragma unroll
@@ -282,13 +288,7 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WP
                 if (!ovalid[r]) continue;
                 chk += v[r];
                 const T f = (ldconst(trow, r) * otz) * ct;  // = ((sx*sy)*sz)*ct, stencil_math analytic
-                if constexpr (FM) {
-                    const T dv = v[r] - f;
-                    ma = max_abs(ma, dv);
-                    mr.add(dv, ldconst(rtw + i * p.tpj, r) * ortz);
-                } else {
-                    accumulate_error_dev(v[r], f, ma, mr);
-                }
+                accumulate_error_dev(v[r], f, ma, mr);
             }
         } else {
 #pragma unroll
@@ -297,6 +297,25 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WP
         }
     };
 
+    // --math fma: branch-free — every own plane, masked lanes and planes outside the error range
+    // contribute d = 0 (the multiplier om * em), so no exec-mask branches and no phi copies of the
+    // running maxima; one scalar load of the (sx sy, 1/|sx sy|) pair per row (txr table)
+    auto errors_fm = [&](const T(&v)[R], const int i, const T ct, T& ma, RelMax<T>& mr, T& chk) {
+        const T em = (i >= p.ei0 && i <= p.ei1) ? T(1) : T(0);
+        const T* const tr = p.txr + 2 * (i * p.tpj + (jt + w * R));
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            chk += ovalid[r] ? v[r] : T(0);
+            const T f = (ldconst(tr, 2 * r) * otz) * ct;  // = ((sx*sy)*sz)*ct
+            const T dv = (v[r] - f) * (om[r] * em);
+            ma = max_abs(ma, dv);
+            mr.add(dv, ldconst(tr, 2 * r + 1) * ortz);
+        }
+    };
+    auto errors = [&](const T(&v)[R], const int i, const T ct, T& ma, Rel& mr, T& chk) {
+        if constexpr (FM) errors_fm(v, i, ct, ma, mr, chk);
+        else errors_exact(v, i, ct, ma, mr, chk);
+    };
     auto plane = [&](auto phase, auto alias, const int i) {
         constexpr int P = decltype(phase)::value;
         constexpr bool ALIAS = decltype(alias)::value;
@@ -638,9 +657,9 @@ template <class T>
 void launch_tb3(int rows, int waves, bool delta, bool fm, bool first, const T* A, const T* B, T* D, T* E,
                 const GridView& gv, const Box* boxes, int nbox, const Box& cdom, int ei0, int ei1,
                 const Wrap& wrapD, const Wrap& wrapE, const SeamPartners<T>& seam, const T* txy,
-                const T* tz, const T* rtxy, const T* rtz, const StepCoefs& cC, const StepCoefs& cD,
+                const T* tz, const T* txr, const T* rtz, const StepCoefs& cC, const StepCoefs& cD,
                 const StepCoefs& cE, u64* errC, u64* errD, u64* errE, int chunk, hipStream_t s) {
-    W3D_REQUIRE(!fm || (rtxy && rtz), "tb3 --math fma needs the reciprocal analytic tables");
+    W3D_REQUIRE(!fm || (txr && rtz), "tb3 --math fma needs the reciprocal analytic tables");
     W3D_REQUIRE(gv.G >= 3, "three-layer temporal blocking needs ghost depth >= 3");
     W3D_REQUIRE(tb3_supported(rows, waves, fm && !delta), "tb3: unsupported rows x waves (x --math fma)");
     W3D_REQUIRE(!delta || tb3_delta_supported(rows, waves, fm), "tb3 increment form: tiles r2w8, r1w8 only");
@@ -672,8 +691,9 @@ void launch_tb3(int rows, int waves, bool delta, bool fm, bool first, const T* A
     p.yx2 = T(1) / T(cC.hx2), p.yy2 = T(1) / T(cC.hy2), p.yz2 = T(1) / T(cC.hz2);
     p.coefC = T(cC.coef), p.coefD = T(cD.coef), p.coefE = T(cE.coef);
     p.ctC = T(cC.ct), p.ctD = T(cD.ct), p.ctE = T(cE.ct);
-    fma_coefs(cC, p.fc[0]), fma_coefs(cD, p.fc[1]), fma_coefs(cE, p.fc[2]);
-    p.rtxy = rtxy, p.rtz = rtz;
+    W3D_REQUIRE(cD.coef == cE.coef && (first || cC.coef == cD.coef), "tb3: layer coefficients differ");
+    fma_coefs(cC, p.fc[0]), fma_coefs(cD, p.fc[1]);
+    p.txr = txr, p.rtz = rtz;
     p.ict[0] = T(1 / std::fabs(cC.ct)), p.ict[1] = T(1 / std::fabs(cD.ct)), p.ict[2] = T(1 / std::fabs(cE.ct));
     p.errC = errC, p.errD = errD, p.errE = errE;
     const int TJ = waves * rows;
