@@ -223,7 +223,10 @@ def test_tb3_fma_sweep_close_to_reference(C, dtype, first, rows, waves, case):
     dD, dE = torch.full(shape, -7.0, dtype=dtype, device=DEV), torch.full(shape, -9.0, dtype=dtype, device=DEV)
     errs = [kernels.new_err(1) for _ in range(3)]
     ei = (min(b[0] for b in boxes), max(b[1] for b in boxes))
-    co = [(*COEF.values(), COEFS[q], CT[q]) for q in range(3)]
+    # the FMA sweep keeps one coefficient triple for the non-first layers (as in a solve, where
+    # every layer but the Taylor start has the same a2 tau^2)
+    coefs = (COEFS[0] if first else COEFS[1], COEFS[1], COEFS[1])
+    co = [(*COEF.values(), coefs[q], CT[q]) for q in range(3)]
     kernels.tb3_sweep(A.to(DEV), B.to(DEV), dD, dE, boxes, first=first, cdom=cdom, err_i=ei,
                       tx=tx.to(DEV), ty=ty.to(DEV), tz=tz.to(DEV), coefs_c=co[0], coefs_d=co[1],
                       coefs_e=co[2], err_c=errs[0], err_d=errs[1], err_e=errs[2], rows=rows,
@@ -231,7 +234,7 @@ def test_tb3_fma_sweep_close_to_reference(C, dtype, first, rows, waves, case):
     torch.cuda.synchronize()
     h = {k: float(v) for k, v in COEF.items()}
     Cf, Df, Ef = reference.chained_layers(A.double(), B.double(), 3, first=first, mask=_mask(shape, G, cdom),
-                                          coefs=list(COEFS), **h)
+                                          coefs=list(coefs), **h)
     tol = dict(rtol=1e-12, atol=1e-12) if dtype == torch.float64 else dict(rtol=2e-5, atol=2e-5)
     gD, gE = dD.cpu(), dE.cpu()
     for b in boxes:
