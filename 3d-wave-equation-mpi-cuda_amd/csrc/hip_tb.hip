@@ -585,6 +585,7 @@ void launch_tb2(int rows, int waves, int occ, int nwk, bool delta, bool fm, bool
                 const T* txr, const T* rtz, const StepCoefs& cC, const StepCoefs& cD, u64* errC, u64* errD,
                 int chunk, hipStream_t s) {
     W3D_REQUIRE(!fm || (txr && rtz), "tb2 --math fma needs the reciprocal analytic tables");
+    W3D_REQUIRE(!fm || first || cC.coef == cD.coef, "tb2 --math fma: the non-first layers must share one coefficient");
     W3D_REQUIRE(gv.G >= 2, "temporal blocking needs ghost depth >= 2");
     W3D_REQUIRE(tb2_supported(rows, waves, occ, nwk), "tb2: unsupported rows x waves x occupancy x k-waves");
     W3D_REQUIRE(!delta || (occ == 0 && tb2_delta_supported(rows, waves, nwk)),

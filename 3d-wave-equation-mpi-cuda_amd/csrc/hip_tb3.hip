@@ -691,7 +691,8 @@ void launch_tb3(int rows, int waves, bool delta, bool fm, bool first, const T* A
     p.yx2 = T(1) / T(cC.hx2), p.yy2 = T(1) / T(cC.hy2), p.yz2 = T(1) / T(cC.hz2);
     p.coefC = T(cC.coef), p.coefD = T(cD.coef), p.coefE = T(cE.coef);
     p.ctC = T(cC.ct), p.ctD = T(cD.ct), p.ctE = T(cE.ct);
-    W3D_REQUIRE(cD.coef == cE.coef && (first || cC.coef == cD.coef), "tb3: layer coefficients differ");
+    W3D_REQUIRE(!fm || (cD.coef == cE.coef && (first || cC.coef == cD.coef)),
+                "tb3 --math fma: the non-first layers must share one coefficient");
     fma_coefs(cC, p.fc[0]), fma_coefs(cD, p.fc[1]);
     p.txr = txr, p.rtz = rtz;
     p.ict[0] = T(1 / std::fabs(cC.ct)), p.ict[1] = T(1 / std::fabs(cD.ct)), p.ict[2] = T(1 / std::fabs(cE.ct));
