@@ -235,10 +235,12 @@ public:
         res.kernel = tb_ ? tb_name(tb_rows_, tb_waves_, tb_occ_, tbd_, tb_nwk_) : kernel_variant_name(kind_);
         res.courant = prob_.courant;
         res.transport = ext_ ? ext_->name() : (world_ > 1 ? "loopback" : "self");
-        // --overlap auto: the first two solves are the trials (on, then off); the arm with the
-        // shorter max-over-ranks solve time is kept for every later solve — the same decision
-        // on every rank, since the times are reduced before the comparison
-        const int trial = overlap_auto_ && trials_done_ < 2 ? trials_done_ : -1;
+        // --overlap auto: solves 2 and 3 are the trials (on, then off; the first solve only warms
+        // up — first launches, RCCL connections of every message shape); the arm with the
+        // shorter max-over-ranks solve time is kept for every later solve — the same decision on
+        // every rank, since the times are reduced before the comparison
+        const int trial = overlap_auto_ && solves_ >= 1 && trials_done_ < 2 ? trials_done_ : -1;
+        ++solves_;
         if (trial >= 0) set_overlap(trial == 0);
         res.overlap = overlap_;
         res.overlap_mode = !(ext_ || world_ > 1) ? "none"
@@ -1714,6 +1716,7 @@ private:
     bool overlap_ = false;
     bool overlap_auto_ = false;   // --overlap auto with a remote halo
     int trials_done_ = 0;         // overlap auto trials run (on, off)
+    int solves_ = 0;              // solves of this session
     double trial_ms_[2] = {0, 0};
     bool xself_ = false;  // --x-self-transport
     static constexpr size_t kMirrorSlots = 2048;

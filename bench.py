@@ -43,7 +43,8 @@ def main() -> int:
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5, help="timed solves")
-    ap.add_argument("--warmup", type=int, default=2, help="untimed solves")
+    ap.add_argument("--warmup", type=int, default=3,
+                    help="untimed solves (with halos, solves 2 and 3 are the --overlap auto trials)")
     ap.add_argument("--N", type=int, default=0, help="override global N (default: the BASELINE config)")
     ap.add_argument("--config", default="",
                     help="run a named BASELINE config instead (models/presets.py CONFIGS, e.g. "

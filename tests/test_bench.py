@@ -100,7 +100,7 @@ def test_bench_gpu_multirank_plan_staged(n, N, dims, golden):
     transport; RCCL refuses duplicate GPUs): each n runs its BASELINE config and decomposition
     at the benchmark's K=100 and must reproduce the reference's golden L-inf; the halo plan is
     verified at setup (halo_checked) and --overlap auto records both trial times."""
-    r = _bench(["--steps", "1", "--warmup", "1", "--transport", "staged", "--shared-device"], nproc=n,
+    r = _bench(["--steps", "1", "--warmup", "2", "--transport", "staged", "--shared-device"], nproc=n,
                timeout=900)
     assert r["n_gpus"] == n and r["config"]["N"] == N and r["config"]["dims"] == dims
     assert r["config"]["transport"] == "staged.gloo" and r["rccl_nranks"] is None
