@@ -18,6 +18,8 @@ std::string usage() {
            "  --dims a,b,c           override the Cartesian process grid\n"
            "  --ranks P              simulate P ranks in-process (loopback transport)\n"
            "  --transport auto|rccl|loopback\n"
+           "  --halo direct|rounds   temporal-blocking deep halos in one round (faces, edges, corners\n"
+           "                         straight from their owners; default) or three dependent rounds\n"
            "  --x-self-transport     one x rank: send the periodic wrap through the transport\n"
            "                         to this rank (exercises RCCL send/recv on a single GPU)\n"
            "  --overlap auto|on|off  interior/shell split with the halo on a second stream; auto\n"
@@ -143,6 +145,11 @@ Config parse_cli(const std::vector<std::string>& a) {
             c.ranks = parse_int(need(i++), "ranks");
         } else if (o == "--transport") {
             c.transport = need(i++);
+        } else if (o == "--halo") {
+            const std::string& v = need(i++);
+            if (v == "direct") c.halo_direct = true;
+            else if (v == "rounds") c.halo_direct = false;
+            else throw Error("wave3d: bad --halo " + v);
         } else if (o == "--x-self-transport") {
             c.x_self_transport = true;
         } else if (o == "--no-overlap") {

@@ -42,6 +42,9 @@ struct Config {
     int check_every = 0;            // >0: abort early when a layer's error is NaN/Inf/>1
     bool strict_cfl = false;        // refuse C > 1/sqrt(3)
     std::string transport = "auto"; // auto | rccl | loopback
+    bool halo_direct = true;        // --halo direct|rounds: deep halos of the temporal-blocking
+                                    // kernels in one round (faces, edges, corners from their owners)
+                                    // or in three dependent rounds (x planes, then y, then z boxes)
     bool x_self_transport = false;  // dims[0] == 1 with an external transport: the periodic
                                     // x wrap travels as messages to this rank (RCCL self
                                     // send/recv) instead of the fused local wrap (testing)

@@ -133,7 +133,7 @@ void launch_tb3(int rows, int waves, bool delta, bool fm, bool first, const T* A
 // Box halo staging for the temporal-blocking exchange on y/z splits: copy the logical box
 // `b` of a level (origin `grid` = logical (0,0,0), strides of `gv`) to / from a contiguous
 // buffer (k fastest). Up to kMaxBoxCopy boxes per launch.
-constexpr int kMaxBoxCopy = 8;
+constexpr int kMaxBoxCopy = 32;
 template <class T>
 struct BoxCopy {
     T* grid = nullptr;

@@ -99,6 +99,10 @@ struct DevRank {
         T* buf;
     };
     std::vector<BoxMsg> tb_bsends[2], tb_brecvs[2];
+    // --halo direct: one round — every face, edge and corner ghost region of the A / B levels
+    // and of the seam alias planes straight from the rank that owns it (level 0 = A, 1 = B,
+    // 2 = alias A, 3 = alias B; box = source region on sends, ghost region on receives)
+    std::vector<BoxMsg> tb_dsends, tb_drecvs;
     T* alias_buf = nullptr;      // one plane: x=N (first x-rank) or x=0 (last x-rank)
     T* alias_bufB = nullptr;     // the same plane of the B level (three-layer blocking)
     T* seamc_buf = nullptr;      // two planes: C on the seam partner planes (three-layer)
@@ -173,6 +177,7 @@ public:
         // test mode: the periodic x wrap of a dims[0] == 1 rank goes through the transport as
         // messages to itself (RCCL send/recv exercised on one GPU), not the fused local wrap
         xself_ = c.x_self_transport;
+        direct_ = c.halo_direct;
         W3D_REQUIRE(!xself_ || ext_, "--x-self-transport needs an external (e.g. RCCL) transport");
         W3D_REQUIRE(!c.rccl_mirror || (!ext_ && world_ > 1), "--rccl-mirror needs simulated ranks (--ranks P)");
     }
@@ -489,6 +494,9 @@ private:
                 for (auto& m : R.tb_bsends[q]) (void)hipFree(m.buf);
                 for (auto& m : R.tb_brecvs[q]) (void)hipFree(m.buf);
             }
+            for (auto* v : {&R.tb_dsends, &R.tb_drecvs}) {
+                for (auto& m : *v) (void)hipFree(m.buf);
+            }
         }
         ranks_.clear();
         if (mirror_buf_) (void)hipFree(mirror_buf_);
@@ -592,6 +600,7 @@ private:
             const bool lastx = t.last(0), firstx = t.first(0);
             const int up = t.nbr[0][1], dn = t.nbr[0][0];
             const bool aliasB = tbd_ == 3;
+            if (direct_) goto x_done;  // single-round plan (build_tb_direct) instead
             R.tb_sends.push_back(M{up, 11, 0, lastx ? X - dA : X - dA + 1, dA});
             if (last) R.tb_sends.push_back(M{up, 12, 0, X, 1});
             R.tb_sends.push_back(M{up, 13, 1, lastx ? X - dB : X - dB + 1, dB});
@@ -608,6 +617,7 @@ private:
             if (last) R.tb_recvs.push_back(M{up, 22, 0, kAliasPlane, 1});
             R.tb_recvs.push_back(M{up, 23, 1, X + 1, dB});
             if (last && aliasB) R.tb_recvs.push_back(M{up, 24, 1, kAliasPlane, 1});
+        x_done:
             if (first || last) {
                 HIP_CHECK(hipMalloc(&R.alias_buf, R.gv.si * sizeof(T)));
                 HIP_CHECK(hipMemset(R.alias_buf, 0, R.gv.si * sizeof(T)));
@@ -619,7 +629,8 @@ private:
         }
         // ---- y (round 0) and z (round 1): next A depth dA, next B depth dB ---------------
         const int G = G_;
-        for (int ax = 1; ax <= 2; ++ax) {
+        if (direct_) build_tb_direct(R);
+        for (int ax = 1; ax <= 2 && !direct_; ++ax) {
             if (t.dims[ax] == 1) continue;
             const int n = ax == 1 ? Y : Z;
             auto box = [&](int lo, int hi) {
@@ -699,12 +710,101 @@ private:
         }
     }
 
+    // Single-round deep-halo plan (--halo direct, the default). The round plan above needs three
+    // dependent rounds (x planes, then y boxes over the received x ghosts, then z boxes over both)
+    // so that edges and corners arrive without diagonal messages. On a fully connected xGMI node
+    // every diagonal neighbour has its own link, so here every ghost region — faces, edges,
+    // corners, of A (depth dA) and B (depth dB), and of the seam alias planes — comes straight
+    // from the rank that owns it, all in one transport group: one latency instead of three, all
+    // links busy at once (2x2x2: 7 peers, one link each). Region rules per axis a, receiver R,
+    // sender S = R + d: d_a = -1 -> R's ghosts 1-D..0 from S's top D owned nodes, +1 -> R's
+    // ghosts E+1..E+D from S's bottom D, 0 -> the owned range (and the x ghosts as well when x
+    // wraps inside the rank: the fused wrap fills them). Across the periodic seam the duplicate
+    // plane is skipped (mpi_new.cpp:186-187): the last x-rank sends X-D..X-1, the first 2..D+1,
+    // and the planes x = N / x = 0 themselves travel as the alias planes. Messages are listed
+    // by (level, direction) on both ends, so per-peer FIFO order matches for tag-less RCCL.
+    void build_tb_direct(DevRank<T>& R) {
+        using BM = typename DevRank<T>::BoxMsg;
+        const auto& t = R.topo;
+        const int E[3] = {t.X(), t.Y(), t.Z()};
+        const int dA = tbd_, dB = tbd_ - 1;
+        const bool selfx = R.plan.self_x;  // dims[0] == 1, wrap fused into the kernels
+        const bool seam = t.dims[0] > 1;   // alias planes exist (first / last x-rank)
+        auto peer = [&](const int d[3]) -> int {  // rank at coords + d, -1 outside y/z
+            int c[3];
+            for (int a = 0; a < 3; ++a) {
+                c[a] = t.coords[a] + d[a];
+                if (a == 0) c[a] = ((c[a] % t.dims[0]) + t.dims[0]) % t.dims[0];
+                else if (c[a] < 0 || c[a] >= t.dims[a]) return -1;
+            }
+            return t.rank_of(c[0], c[1], c[2]);
+        };
+        auto add = [&](std::vector<BM>& v, int pr, int tag, int level, Box b) {
+            T* buf = nullptr;
+            HIP_CHECK(hipMalloc(&buf, size_t(b.count()) * sizeof(T)));
+            v.push_back(BM{pr, tag, level, b, buf});
+        };
+        // receive box of R for direction d (ghost region), depth D
+        auto rbox = [&](const int d[3], int D, bool alias) {
+            int lo[3], hi[3];
+            for (int a = 0; a < 3; ++a) {
+                if (d[a] < 0) lo[a] = 1 - D, hi[a] = 0;
+                else if (d[a] > 0) lo[a] = E[a] + 1, hi[a] = E[a] + D;
+                else if (a == 0 && selfx) lo[a] = 1 - D, hi[a] = E[a] + D;
+                else lo[a] = 1, hi[a] = E[a];
+            }
+            if (alias) lo[0] = hi[0] = 0;  // the alias buffer's one plane (logical i = 0)
+            return Box{lo[0], hi[0], lo[1], hi[1], lo[2], hi[2]};
+        };
+        // source box of R for a receiver Q = R - d (R fills Q's ghosts in direction d)
+        auto sbox = [&](const int d[3], int D, bool alias) {
+            int lo[3], hi[3];
+            for (int a = 0; a < 3; ++a) {
+                // crossing the periodic seam from Q to R: Q first and R last x-rank (d = -1),
+                // or Q last and R first (d = +1); with one x rank messaging itself both hold
+                const int tw = a == 0 && ((d[a] < 0 && t.last(0)) || (d[a] > 0 && t.first(0))) ? 1 : 0;
+                if (d[a] < 0) lo[a] = E[a] - D + 1 - tw, hi[a] = E[a] - tw;
+                else if (d[a] > 0) lo[a] = 1 + tw, hi[a] = D + tw;
+                else if (a == 0 && selfx) lo[a] = 1 - D, hi[a] = E[a] + D;
+                else lo[a] = 1, hi[a] = E[a];
+            }
+            if (alias) lo[0] = hi[0] = d[0] < 0 ? E[0] : 1;  // plane x = N (last) / x = 0 (first)
+            return Box{lo[0], hi[0], lo[1], hi[1], lo[2], hi[2]};
+        };
+        for (int level = 0; level < (tbd_ == 3 ? 4 : 3); ++level) {
+            const bool alias = level >= 2;
+            if (alias && !seam) continue;
+            const int D = (level == 0 || level == 2) ? dA : dB;
+            int q = 0;
+            for (int dx = -1; dx <= 1; ++dx)
+                for (int dy = -1; dy <= 1; ++dy)
+                    for (int dz = -1; dz <= 1; ++dz, ++q) {
+                        if (!dx && !dy && !dz) continue;
+                        if (selfx && dx) continue;  // x ghosts: fused wrap
+                        if (alias && !dx) continue;  // alias planes cross the x seam only
+                        const int tag = 200 + q * 4 + level;
+                        const int d[3] = {dx, dy, dz}, md[3] = {-dx, -dy, -dz};
+                        // receive: from S = R + d into R's ghosts (alias: R first x-rank <- last
+                        // for d_x = -1, R last <- first for d_x = +1)
+                        const int S = peer(d);
+                        const bool ra = !alias || (dx < 0 ? t.first(0) : t.last(0));
+                        if (S >= 0 && ra) add(R.tb_drecvs, S, tag, level, rbox(d, D, alias));
+                        // send: to Q = R - d from R's own nodes (alias: R last x-rank -> first
+                        // for d_x = -1, R first -> last for d_x = +1)
+                        const int Q = peer(md);
+                        const bool sa = !alias || (dx < 0 ? t.last(0) : t.first(0));
+                        if (Q >= 0 && sa) add(R.tb_dsends, Q, tag, level, sbox(d, D, alias));
+                    }
+        }
+    }
+
     // single-step overlap: y/z shells as whole tiles of the march kernel (else flat shells)
     bool shells_tiled() const { return kind_.march && !kind_.flat; }
 
     bool tb_halo(const DevRank<T>& R) const {
         return !R.tb_sends.empty() || !R.tb_bsends[0].empty() || !R.tb_bsends[1].empty() ||
-               !R.tb_brecvs[0].empty() || !R.tb_brecvs[1].empty();
+               !R.tb_brecvs[0].empty() || !R.tb_brecvs[1].empty() || !R.tb_dsends.empty() ||
+               !R.tb_drecvs.empty();
     }
 
     void* tb_ptr(DevRank<T>& R, const typename DevRank<T>::PlaneMsg& m, int mD) {
@@ -713,7 +813,56 @@ private:
     }
 
     // exchange after a sweep whose D layer is mD (A level = mD, B level = mD-1)
+    // --halo direct: pack every message, one transport group (or loopback copies), unpack
+    T* direct_grid(DevRank<T>& R, int level, int mD) {
+        if (level == 2) return R.alias_buf + R.plane_off;
+        if (level == 3) return R.alias_bufB + R.plane_off;
+        return R.g[lvl(level == 0 ? mD : mD - 1 + L_)];
+    }
+    void box_copies(DevRank<T>& R, std::vector<typename DevRank<T>::BoxMsg>& v, int mD, bool to_buf, hipStream_t s) {
+        for (size_t q0 = 0; q0 < v.size(); q0 += kMaxBoxCopy) {
+            BoxCopy<T> o[kMaxBoxCopy];
+            int n = 0;
+            for (size_t q = q0; q < v.size() && n < kMaxBoxCopy; ++q, ++n)
+                o[n].grid = direct_grid(R, v[q].level, mD), o[n].buf = v[q].buf, o[n].b = v[q].box;
+            launch_box_copy<T>(o, n, R.gv, to_buf, s);
+        }
+    }
+    void exchange_direct(int mD, hipStream_t s) {
+        for (auto& R : ranks_) box_copies(R, R.tb_dsends, mD, true, s);
+        auto bytes = [](const typename DevRank<T>::BoxMsg& m) { return size_t(m.box.count()) * sizeof(T); };
+        mark(s, 6);
+        if (ext_) {
+            auto& R = ranks_[0];
+            std::vector<Message> snd, rcv;
+            for (auto& m : R.tb_dsends) snd.push_back({m.peer, m.tag, m.buf, bytes(m)});
+            for (auto& m : R.tb_drecvs) rcv.push_back({m.peer, m.tag, m.buf, bytes(m)});
+            if (!snd.empty() || !rcv.empty()) ext_->exchange(snd, rcv, s);
+        } else {
+            for (auto& S : ranks_)
+                for (auto& m : S.tb_dsends) {
+                    bool done = false;
+                    for (auto& g : ranks_[m.peer].tb_drecvs)
+                        if (g.peer == S.topo.rank && g.tag == m.tag) {
+                            W3D_REQUIRE(bytes(g) == bytes(m), "direct halo size mismatch (tag " +
+                                                                  std::to_string(m.tag) + ")");
+                            loop_copy(g.buf, m.buf, bytes(m), S.topo.rank, m.peer, m.tag, s);
+                            done = true;
+                            break;
+                        }
+                    W3D_REQUIRE(done, "unmatched direct halo message (tag " + std::to_string(m.tag) + ")");
+                }
+        }
+        mark(s, 7);
+        for (auto& R : ranks_) box_copies(R, R.tb_drecvs, mD, false, s);
+        for (auto& R : ranks_) inject_after_exchange(R, mD, s);
+    }
+
     void exchange_tb(int mD, hipStream_t s) {
+        if (direct_) {
+            exchange_direct(mD, s);
+            return;
+        }
         if (ext_) {
             auto& R = ranks_[0];
             std::vector<Message> snd, rcv;
@@ -996,6 +1145,7 @@ private:
             for (auto& m : R.tb_sends) most = std::max(most, size_t(m.nplanes) * size_t(R.gv.si) * sizeof(T));
             for (int rd = 0; rd < 2; ++rd)
                 for (auto& m : R.tb_bsends[rd]) most = std::max(most, size_t(m.box.count()) * sizeof(T));
+            for (auto& m : R.tb_dsends) most = std::max(most, size_t(m.box.count()) * sizeof(T));
         }
         int dev = 0;
         HIP_CHECK(hipGetDevice(&dev));
@@ -1082,6 +1232,14 @@ private:
                 region(m.peer, m.tag, R.g[m.level == 0 ? lA : lB],
                        Box{m.plane, m.plane + m.nplanes - 1, 1, Y, 1, Z}, salt, -1, "x planes");
             }
+        }
+        for (const auto& m : R.tb_drecvs) {  // --halo direct: every message is one box
+            Box b = m.box;
+            if (R.plan.self_x && m.level < 2) b.i0 = std::max(b.i0, 1), b.i1 = std::min(b.i1, X);
+            const unsigned salt = (m.level == 0 || m.level == 2) ? sA : sB;
+            const bool al = m.level >= 2;
+            region(m.peer, m.tag, direct_grid(R, m.level, 2), b, salt, al ? alias_gi : -1,
+                   al ? "direct alias box" : "direct box");
         }
         const int dA = tbd_, dB = tbd_ - 1;
         for (int rd = 0; rd < 2; ++rd)
@@ -1719,6 +1877,7 @@ private:
     int solves_ = 0;              // solves of this session
     double trial_ms_[2] = {0, 0};
     bool xself_ = false;  // --x-self-transport
+    bool direct_ = true;  // --halo direct: single-round deep-halo plan (build_tb_direct)
     static constexpr size_t kMirrorSlots = 2048;
     std::unique_ptr<RcclTransport> mirror_;  // --rccl-mirror: 1-rank communicator
     void* mirror_buf_ = nullptr;

@@ -16,41 +16,49 @@ pytestmark = pytest.mark.gpu
 ARGS = ["40", "1", "pi", "pi", "pi", "1", "12"]
 
 CASES = [
-    # (dims, kernel, dtype, a tag the plan delivers to rank 1)
-    ("2,1,1", "march2", "fp64", 1),
-    ("2,2,2", "march2", "fp64", 4),
-    ("1,2,2", "march2", "fp64", 5),
-    ("2,1,1", "tb2", "fp64", 11),
-    ("2,2,2", "tb2", "fp64", 61),
-    ("1,2,2", "tb2", "fp64", 32),
-    ("4,1,1", "tb3", "fp64", 13),
-    ("2,2,2", "tb3", "fp32", 63),
-    ("1,2,2", "tb3", "fp32", 31),
+    # (dims, kernel, dtype, a tag the plan delivers to rank 1, deep-halo plan)
+    ("2,1,1", "march2", "fp64", 1, "direct"),
+    ("2,2,2", "march2", "fp64", 4, "direct"),
+    ("1,2,2", "march2", "fp64", 5, "direct"),
+    ("2,1,1", "tb2", "fp64", 11, "rounds"),
+    ("2,2,2", "tb2", "fp64", 61, "rounds"),
+    ("1,2,2", "tb2", "fp64", 32, "rounds"),
+    ("4,1,1", "tb3", "fp64", 13, "rounds"),
+    ("2,2,2", "tb3", "fp32", 63, "rounds"),
+    ("1,2,2", "tb3", "fp32", 31, "rounds"),
+    # --halo direct (default): tag = 200 + 4 * direction + level, direction = 9(dx+1)+3(dy+1)+(dz+1)
+    ("2,1,1", "tb2", "fp64", 216, "direct"),   # x face (-1,0,0), level A
+    ("2,1,1", "tb2", "fp64", 290, "direct"),   # seam alias plane from the first x-rank (+1,0,0)
+    ("2,2,2", "tb2", "fp64", 296, "direct"),   # corner (+1,+1,-1), level A
+    ("1,2,2", "tb3", "fp32", 261, "direct"),   # y/z edge (0,+1,-1), level B, x ghosts by wrap
+    ("2,2,2", "tb3", "fp64", 226, "direct"),   # alias A corner (-1,+1,-1)
+    ("2,2,2", "tb3", "fp64", 227, "direct"),   # alias B corner (-1,+1,-1)
+    ("4,1,1", "tb3r1w8", "fp64", 217, "direct"),
 ]
 
 
-def _run(gpu_prog, dims, kernel, dtype, extra=()):
+def _run(gpu_prog, dims, kernel, dtype, extra=(), halo="direct"):
     P = 1
     for d in dims.split(","):
         P *= int(d)
     cmd = [gpu_prog] + ARGS + ["--ranks", str(P), "--dims", dims, "--kernel", kernel, "--dtype", dtype,
-                               "--json", "--quiet", "--format", "none"] + list(extra)
+                               "--halo", halo, "--json", "--quiet", "--format", "none"] + list(extra)
     t0 = time.time()
     out = subprocess.run(cmd, capture_output=True, text=True, timeout=120)
     return out, time.time() - t0
 
 
-@pytest.mark.parametrize("dims,kernel,dtype,tag", CASES)
-def test_halo_selftest_passes(gpu_prog, dims, kernel, dtype, tag):
-    out, _ = _run(gpu_prog, dims, kernel, dtype)
+@pytest.mark.parametrize("dims,kernel,dtype,tag,halo", CASES)
+def test_halo_selftest_passes(gpu_prog, dims, kernel, dtype, tag, halo):
+    out, _ = _run(gpu_prog, dims, kernel, dtype, halo=halo)
     assert out.returncode == 0, out.stderr[-2000:]
     r = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][0])
     assert r["halo_checked"] > 0 and r["kernel"].startswith(kernel[:3])
 
 
-@pytest.mark.parametrize("dims,kernel,dtype,tag", CASES)
-def test_halo_selftest_names_corrupted_tag(gpu_prog, dims, kernel, dtype, tag):
-    out, dt = _run(gpu_prog, dims, kernel, dtype, ["--fault", f"corrupt_tag:1:{tag}"])
+@pytest.mark.parametrize("dims,kernel,dtype,tag,halo", CASES)
+def test_halo_selftest_names_corrupted_tag(gpu_prog, dims, kernel, dtype, tag, halo):
+    out, dt = _run(gpu_prog, dims, kernel, dtype, ["--fault", f"corrupt_tag:1:{tag}"], halo=halo)
     assert out.returncode != 0
     assert "halo self-test failed" in out.stderr, out.stderr[-2000:]
     assert f"rank 1: message from peer" in out.stderr and f" tag {tag} " in out.stderr, out.stderr[-2000:]
@@ -58,7 +66,7 @@ def test_halo_selftest_names_corrupted_tag(gpu_prog, dims, kernel, dtype, tag):
 
 
 def test_halo_selftest_can_be_skipped(gpu_prog):
-    out, _ = _run(gpu_prog, "2,1,1", "tb2", "fp64", ["--no-halo-check", "--fault", "corrupt_tag:1:11"])
+    out, _ = _run(gpu_prog, "2,1,1", "tb2", "fp64", ["--no-halo-check", "--fault", "corrupt_tag:1:216"])
     assert out.returncode == 0, out.stderr[-2000:]
     r = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][0])
     assert r["halo_checked"] == 0
@@ -70,12 +78,13 @@ MIRROR = [("2,2,2", "tb2", "fp64"), ("1,2,2", "tb2", "fp64"), ("2,2,2", "tb3", "
 
 @pytest.mark.parametrize("dims,kernel,dtype", MIRROR)
 @pytest.mark.parametrize("overlap", ["on", "off"])
-def test_rccl_mirror_every_message_shape(gpu_prog, cpu_prog, dims, kernel, dtype, overlap):
+@pytest.mark.parametrize("halo", ["direct", "rounds"])
+def test_rccl_mirror_every_message_shape(gpu_prog, cpu_prog, dims, kernel, dtype, overlap, halo):
     """--rccl-mirror: every halo message of the multi-GPU plan (x planes, seam alias planes,
     y/z box rounds, faces) and the error-key allreduce also run through a 1-rank RCCL
     communicator and are compared bitwise on the device with the loopback copy; the per-layer
     errors equal the OpenMP oracle's (same decomposition)."""
-    out, _ = _run(gpu_prog, dims, kernel, dtype, ["--rccl-mirror", "--overlap", overlap, "--repeat", "2"])
+    out, _ = _run(gpu_prog, dims, kernel, dtype, ["--rccl-mirror", "--overlap", overlap, "--repeat", "2"], halo=halo)
     assert out.returncode == 0, out.stderr[-3000:]
     r = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][0])
     assert r["rccl_mirror_msgs"] > 0 and r["halo_checked"] > 0 and r["overlap"] == (overlap == "on")

@@ -396,7 +396,8 @@ def test_fp32_auto_is_tb3_bitwise(C):
                                            ("tb2", "delta")])
 @pytest.mark.parametrize("dims", ["2,2,2", "1,2,2"])
 @pytest.mark.parametrize("K", [40, 41])
-def test_overlap_concurrent_interior_bitwise(C, kernel, scheme, dims, K):
+@pytest.mark.parametrize("halo", ["direct", "rounds"])
+def test_overlap_concurrent_interior_bitwise(C, kernel, scheme, dims, K, halo):
     """Overlap on a grid large enough that the tile-aligned interior is non-empty (N=160: the
     interior sweep really runs concurrently with the shells on the comm stream), on the 3-D
     block decompositions, odd and even K: bitwise equal to the OpenMP oracle."""
@@ -405,7 +406,9 @@ def test_overlap_concurrent_interior_bitwise(C, kernel, scheme, dims, K):
     p = wave3d.WaveProblem(160, Lx=1.3, Ly="pi", Lz=2.0, timesteps=K, ic="shifted", scheme=scheme)
     assert p.stable()
     d = [int(x) for x in dims.split(",")]
-    r = _solve(p, ranks=d[0] * d[1] * d[2], dims=d, overlap=True, kernel=kernel)
+    s = wave3d.WaveSolver(p, "hip", ranks=d[0] * d[1] * d[2], dims=d, overlap=True, kernel=kernel)
+    s.opts["halo"] = halo
+    r = s.run()
     assert r.extra["overlap"] is True and r.extra["overlap_interior"] > 0
     ref = _solve(p, backend="cpu", threads=8)
     assert r.max_abs == ref.max_abs and r.max_rel == ref.max_rel
