@@ -813,18 +813,25 @@ private:
     }
 
     // exchange after a sweep whose D layer is mD (A level = mD, B level = mD-1)
-    // --halo direct: pack every message, one transport group (or loopback copies), unpack
-    T* direct_grid(DevRank<T>& R, int level, int mD) {
-        if (level == 2) return R.alias_buf + R.plane_off;
-        if (level == 3) return R.alias_bufB + R.plane_off;
-        return R.g[lvl(level == 0 ? mD : mD - 1 + L_)];
+    // --halo direct: pack every message, one transport group (or loopback copies), unpack.
+    // Grid of a message's box: levels 0 / 1 are the A / B levels; the seam alias levels 2 / 3 are
+    // sent from the sender's own A / B planes (x = N or x = 0) and received into the alias
+    // buffers (one plane, logical i = 0).
+    T* direct_grid(DevRank<T>& R, int level, int mD, bool send) {
+        if (level == 2 && !send) return R.alias_buf + R.plane_off;
+        if (level == 3 && !send) return R.alias_bufB + R.plane_off;
+        return R.g[lvl(level % 2 == 0 ? mD : mD - 1 + L_)];
     }
     void box_copies(DevRank<T>& R, std::vector<typename DevRank<T>::BoxMsg>& v, int mD, bool to_buf, hipStream_t s) {
         for (size_t q0 = 0; q0 < v.size(); q0 += kMaxBoxCopy) {
             BoxCopy<T> o[kMaxBoxCopy];
             int n = 0;
-            for (size_t q = q0; q < v.size() && n < kMaxBoxCopy; ++q, ++n)
-                o[n].grid = direct_grid(R, v[q].level, mD), o[n].buf = v[q].buf, o[n].b = v[q].box;
+            for (size_t q = q0; q < v.size() && n < kMaxBoxCopy; ++q, ++n) {
+                // an alias buffer holds one plane: never let a box index another (host check)
+                W3D_REQUIRE(v[q].level < 2 || to_buf || (v[q].box.i0 == 0 && v[q].box.i1 == 0),
+                            "direct halo: alias box outside its one-plane buffer");
+                o[n].grid = direct_grid(R, v[q].level, mD, to_buf), o[n].buf = v[q].buf, o[n].b = v[q].box;
+            }
             launch_box_copy<T>(o, n, R.gv, to_buf, s);
         }
     }
@@ -1238,7 +1245,7 @@ private:
             if (R.plan.self_x && m.level < 2) b.i0 = std::max(b.i0, 1), b.i1 = std::min(b.i1, X);
             const unsigned salt = (m.level == 0 || m.level == 2) ? sA : sB;
             const bool al = m.level >= 2;
-            region(m.peer, m.tag, direct_grid(R, m.level, 2), b, salt, al ? alias_gi : -1,
+            region(m.peer, m.tag, direct_grid(R, m.level, 2, false), b, salt, al ? alias_gi : -1,
                    al ? "direct alias box" : "direct box");
         }
         const int dA = tbd_, dB = tbd_ - 1;
