@@ -103,6 +103,14 @@ struct DevRank {
     // and of the seam alias planes straight from the rank that owns it (level 0 = A, 1 = B,
     // 2 = alias A, 3 = alias B; box = source region on sends, ghost region on receives)
     std::vector<BoxMsg> tb_dsends, tb_drecvs;
+    // ... packed back to back per peer: one message per peer and direction of travel (2x2x2:
+    // 7 peers, one xGMI link each); BoxMsg::buf points into these
+    struct PeerBuf {
+        int peer;
+        T* buf;
+        size_t count;
+    };
+    std::vector<PeerBuf> tb_psends, tb_precvs;
     T* alias_buf = nullptr;      // one plane: x=N (first x-rank) or x=0 (last x-rank)
     T* alias_bufB = nullptr;     // the same plane of the B level (three-layer blocking)
     T* seamc_buf = nullptr;      // two planes: C on the seam partner planes (three-layer)
@@ -494,7 +502,7 @@ private:
                 for (auto& m : R.tb_bsends[q]) (void)hipFree(m.buf);
                 for (auto& m : R.tb_brecvs[q]) (void)hipFree(m.buf);
             }
-            for (auto* v : {&R.tb_dsends, &R.tb_drecvs}) {
+            for (auto* v : {&R.tb_psends, &R.tb_precvs}) {
                 for (auto& m : *v) (void)hipFree(m.buf);
             }
         }
@@ -740,9 +748,7 @@ private:
             return t.rank_of(c[0], c[1], c[2]);
         };
         auto add = [&](std::vector<BM>& v, int pr, int tag, int level, Box b) {
-            T* buf = nullptr;
-            HIP_CHECK(hipMalloc(&buf, size_t(b.count()) * sizeof(T)));
-            v.push_back(BM{pr, tag, level, b, buf});
+            v.push_back(BM{pr, tag, level, b, nullptr});  // buffer: the peer's packed message
         };
         // receive box of R for direction d (ghost region), depth D
         auto rbox = [&](const int d[3], int D, bool alias) {
@@ -796,6 +802,27 @@ private:
                         if (Q >= 0 && sa) add(R.tb_dsends, Q, tag, level, sbox(d, D, alias));
                     }
         }
+        // one buffer per peer: its boxes back to back in (level, direction) order — the order
+        // in which both ends list them, so the packed messages have the same layout
+        auto aggregate = [&](std::vector<BM>& v, std::vector<typename DevRank<T>::PeerBuf>& agg) {
+            std::vector<int> peers;
+            for (auto& m : v)
+                if (std::find(peers.begin(), peers.end(), m.peer) == peers.end()) peers.push_back(m.peer);
+            std::sort(peers.begin(), peers.end());
+            for (int pr : peers) {
+                size_t n = 0;
+                for (auto& m : v)
+                    if (m.peer == pr) n += size_t(m.box.count());
+                T* buf = nullptr;
+                HIP_CHECK(hipMalloc(&buf, n * sizeof(T)));
+                size_t off = 0;
+                for (auto& m : v)
+                    if (m.peer == pr) m.buf = buf + off, off += size_t(m.box.count());
+                agg.push_back({pr, buf, n});
+            }
+        };
+        aggregate(R.tb_dsends, R.tb_psends);
+        aggregate(R.tb_drecvs, R.tb_precvs);
     }
 
     // single-step overlap: y/z shells as whole tiles of the march kernel (else flat shells)
@@ -839,25 +866,28 @@ private:
         for (auto& R : ranks_) box_copies(R, R.tb_dsends, mD, true, s);
         auto bytes = [](const typename DevRank<T>::BoxMsg& m) { return size_t(m.box.count()) * sizeof(T); };
         mark(s, 6);
+        (void)bytes;
+        constexpr int kPeerTag = 199;  // one packed message per peer and direction of travel
         if (ext_) {
             auto& R = ranks_[0];
             std::vector<Message> snd, rcv;
-            for (auto& m : R.tb_dsends) snd.push_back({m.peer, m.tag, m.buf, bytes(m)});
-            for (auto& m : R.tb_drecvs) rcv.push_back({m.peer, m.tag, m.buf, bytes(m)});
+            for (auto& m : R.tb_psends) snd.push_back({m.peer, kPeerTag, m.buf, m.count * sizeof(T)});
+            for (auto& m : R.tb_precvs) rcv.push_back({m.peer, kPeerTag, m.buf, m.count * sizeof(T)});
             if (!snd.empty() || !rcv.empty()) ext_->exchange(snd, rcv, s);
         } else {
             for (auto& S : ranks_)
-                for (auto& m : S.tb_dsends) {
+                for (auto& m : S.tb_psends) {
                     bool done = false;
-                    for (auto& g : ranks_[m.peer].tb_drecvs)
-                        if (g.peer == S.topo.rank && g.tag == m.tag) {
-                            W3D_REQUIRE(bytes(g) == bytes(m), "direct halo size mismatch (tag " +
-                                                                  std::to_string(m.tag) + ")");
-                            loop_copy(g.buf, m.buf, bytes(m), S.topo.rank, m.peer, m.tag, s);
+                    for (auto& g : ranks_[m.peer].tb_precvs)
+                        if (g.peer == S.topo.rank) {
+                            W3D_REQUIRE(g.count == m.count, "direct halo size mismatch between ranks " +
+                                                                std::to_string(S.topo.rank) + " and " +
+                                                                std::to_string(m.peer));
+                            loop_copy(g.buf, m.buf, m.count * sizeof(T), S.topo.rank, m.peer, kPeerTag, s);
                             done = true;
                             break;
                         }
-                    W3D_REQUIRE(done, "unmatched direct halo message (tag " + std::to_string(m.tag) + ")");
+                    W3D_REQUIRE(done, "unmatched direct halo message to rank " + std::to_string(m.peer));
                 }
         }
         mark(s, 7);
@@ -1152,7 +1182,7 @@ private:
             for (auto& m : R.tb_sends) most = std::max(most, size_t(m.nplanes) * size_t(R.gv.si) * sizeof(T));
             for (int rd = 0; rd < 2; ++rd)
                 for (auto& m : R.tb_bsends[rd]) most = std::max(most, size_t(m.box.count()) * sizeof(T));
-            for (auto& m : R.tb_dsends) most = std::max(most, size_t(m.box.count()) * sizeof(T));
+            for (auto& m : R.tb_psends) most = std::max(most, m.count * sizeof(T));
         }
         int dev = 0;
         HIP_CHECK(hipGetDevice(&dev));
