@@ -608,7 +608,6 @@ private:
             const bool lastx = t.last(0), firstx = t.first(0);
             const int up = t.nbr[0][1], dn = t.nbr[0][0];
             const bool aliasB = tbd_ == 3;
-            if (direct_) goto x_done;  // single-round plan (build_tb_direct) instead
             R.tb_sends.push_back(M{up, 11, 0, lastx ? X - dA : X - dA + 1, dA});
             if (last) R.tb_sends.push_back(M{up, 12, 0, X, 1});
             R.tb_sends.push_back(M{up, 13, 1, lastx ? X - dB : X - dB + 1, dB});
@@ -625,7 +624,6 @@ private:
             if (last) R.tb_recvs.push_back(M{up, 22, 0, kAliasPlane, 1});
             R.tb_recvs.push_back(M{up, 23, 1, X + 1, dB});
             if (last && aliasB) R.tb_recvs.push_back(M{up, 24, 1, kAliasPlane, 1});
-        x_done:
             if (first || last) {
                 HIP_CHECK(hipMalloc(&R.alias_buf, R.gv.si * sizeof(T)));
                 HIP_CHECK(hipMemset(R.alias_buf, 0, R.gv.si * sizeof(T)));
@@ -788,6 +786,7 @@ private:
                         if (!dx && !dy && !dz) continue;
                         if (selfx && dx) continue;  // x ghosts: fused wrap
                         if (alias && !dx) continue;  // alias planes cross the x seam only
+                        if (!dy && !dz) continue;    // x faces: whole planes in place (x list)
                         const int tag = 200 + q * 4 + level;
                         const int d[3] = {dx, dy, dz}, md[3] = {-dx, -dy, -dz};
                         // receive: from S = R + d into R's ghosts (alias: R first x-rank <- last
@@ -869,12 +868,33 @@ private:
         (void)bytes;
         constexpr int kPeerTag = 199;  // one packed message per peer and direction of travel
         if (ext_) {
+            // x faces as whole planes sent and received in place (their y/z ghost rows are
+            // overwritten by the edge boxes unpacked after the group), then one packed message
+            // per peer — the same order on both ends
             auto& R = ranks_[0];
             std::vector<Message> snd, rcv;
+            for (auto& m : R.tb_sends)
+                snd.push_back({m.peer, m.tag, tb_ptr(R, m, mD), size_t(m.nplanes) * R.gv.si * sizeof(T)});
+            for (auto& m : R.tb_recvs)
+                rcv.push_back({m.peer, m.tag, tb_ptr(R, m, mD), size_t(m.nplanes) * R.gv.si * sizeof(T)});
             for (auto& m : R.tb_psends) snd.push_back({m.peer, kPeerTag, m.buf, m.count * sizeof(T)});
             for (auto& m : R.tb_precvs) rcv.push_back({m.peer, kPeerTag, m.buf, m.count * sizeof(T)});
             if (!snd.empty() || !rcv.empty()) ext_->exchange(snd, rcv, s);
         } else {
+            for (auto& S : ranks_)
+                for (auto& m : S.tb_sends) {
+                    auto& D = ranks_[m.peer];
+                    bool done = false;
+                    for (auto& g : D.tb_recvs)
+                        if (g.peer == S.topo.rank && g.tag == m.tag) {
+                            W3D_REQUIRE(g.nplanes == m.nplanes, "tb halo size mismatch");
+                            loop_copy(tb_ptr(D, g, mD), tb_ptr(S, m, mD), size_t(m.nplanes) * S.gv.si * sizeof(T),
+                                      S.topo.rank, D.topo.rank, m.tag, s);
+                            done = true;
+                            break;
+                        }
+                    W3D_REQUIRE(done, "unmatched tb halo message");
+                }
             for (auto& S : ranks_)
                 for (auto& m : S.tb_psends) {
                     bool done = false;

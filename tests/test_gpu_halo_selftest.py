@@ -26,14 +26,15 @@ CASES = [
     ("4,1,1", "tb3", "fp64", 13, "rounds"),
     ("2,2,2", "tb3", "fp32", 63, "rounds"),
     ("1,2,2", "tb3", "fp32", 31, "rounds"),
-    # --halo direct (default): tag = 200 + 4 * direction + level, direction = 9(dx+1)+3(dy+1)+(dz+1)
-    ("2,1,1", "tb2", "fp64", 216, "direct"),   # x face (-1,0,0), level A
-    ("2,1,1", "tb2", "fp64", 290, "direct"),   # seam alias plane from the first x-rank (+1,0,0)
+    # --halo direct (default): x faces as whole planes in place (the x round's tags); edges, corners
+    # and y/z faces packed, tag = 200 + 4 * direction + level, direction = 9(dx+1)+3(dy+1)+(dz+1)
+    ("2,1,1", "tb2", "fp64", 11, "direct"),    # x face planes, in place (as the x round)
+    ("2,1,1", "tb2", "fp64", 22, "direct"),    # seam alias plane from the first x-rank
     ("2,2,2", "tb2", "fp64", 296, "direct"),   # corner (+1,+1,-1), level A
     ("1,2,2", "tb3", "fp32", 261, "direct"),   # y/z edge (0,+1,-1), level B, x ghosts by wrap
     ("2,2,2", "tb3", "fp64", 226, "direct"),   # alias A corner (-1,+1,-1)
     ("2,2,2", "tb3", "fp64", 227, "direct"),   # alias B corner (-1,+1,-1)
-    ("4,1,1", "tb3r1w8", "fp64", 217, "direct"),
+    ("4,1,1", "tb3r1w8", "fp64", 13, "direct"),   # x face planes of the B level
 ]
 
 
@@ -66,7 +67,7 @@ def test_halo_selftest_names_corrupted_tag(gpu_prog, dims, kernel, dtype, tag, h
 
 
 def test_halo_selftest_can_be_skipped(gpu_prog):
-    out, _ = _run(gpu_prog, "2,1,1", "tb2", "fp64", ["--no-halo-check", "--fault", "corrupt_tag:1:216"])
+    out, _ = _run(gpu_prog, "2,1,1", "tb2", "fp64", ["--no-halo-check", "--fault", "corrupt_tag:1:11"])
     assert out.returncode == 0, out.stderr[-2000:]
     r = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][0])
     assert r["halo_checked"] == 0
