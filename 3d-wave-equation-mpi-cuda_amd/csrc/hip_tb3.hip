@@ -31,6 +31,12 @@
 
 #include "device_common.hpp"
 
+// timing ablations of the sweep (tools/ab_tb3_abl.sh builds; never the shipped library):
+// 1 = no error accumulation, 2 = errors without the analytic-table loads, 3 = no ring C/D
+#ifndef W3D_TB3_ABL
+#define W3D_TB3_ABL 0
+#endif
+
 namespace wave3d {
 namespace {
 
@@ -301,30 +307,45 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WP
     // contribute d = 0 (the multiplier om * em), so no exec-mask branches and no phi copies of the
     // running maxima; one scalar load of the (sx sy, 1/|sx sy|) pair per row (txr table)
     auto errors_fm = [&](const T(&v)[R], const int i, const T ct, T& ma, RelMax<T>& mr, T& chk) {
+#if W3D_TB3_ABL == 1
+        return;
+#endif
         const T em = (i >= p.ei0 && i <= p.ei1) ? T(1) : T(0);
         const T* const tr = p.txr + 2 * (i * p.tpj + (jt + w * R));
 #pragma unroll
         for (int r = 0; r < R; ++r) {
             chk += ovalid[r] ? v[r] : T(0);
+#if W3D_TB3_ABL == 2
+            const T f = (T(0.5) * otz) * ct;
+            const T dv = (v[r] - f) * (om[r] * em);
+            ma = max_abs(ma, dv);
+            mr.add(dv, T(0.25) * ortz);
+#else
             const T f = (ldconst(tr, 2 * r) * otz) * ct;  // = ((sx*sy)*sz)*ct
             const T dv = (v[r] - f) * (om[r] * em);
             ma = max_abs(ma, dv);
             mr.add(dv, ldconst(tr, 2 * r + 1) * ortz);
+#endif
         }
     };
     auto errors = [&](const T(&v)[R], const int i, const T ct, T& ma, Rel& mr, T& chk) {
         if constexpr (FM) errors_fm(v, i, ct, ma, mr, chk);
         else errors_exact(v, i, ct, ma, mr, chk);
     };
+    // SLOW (ALIAS): the prologue / epilogue planes of the work item and the periodic seam
+    // planes — every range check and the seam partners. FAST: the steady state (planes
+    // ib+2 .. ie off the seam), where C(i), D(i-1) and E(i-2) are all own planes and the
+    // prefetch is live, so the body has no range tests (fewer scalar branches per plane).
     auto plane = [&](auto phase, auto alias, const int i) {
         constexpr int P = decltype(phase)::value;
         constexpr bool ALIAS = decltype(alias)::value;
+        constexpr bool FAST = !ALIAS;
         constexpr int S0 = P & 3, S1 = (P + 1) & 3, S2 = (P + 2) & 3, S3 = (P + 3) & 3;
         constexpr int H0 = P & 1, H1 = (P + 1) & 1;
 
         // ---- prefetch A(i+2), B(i+1) (own and ring; 0-record descriptors when done) --------
         {
-            const bool more = i <= ie + 1;
+            const bool more = FAST || i <= ie + 1;
             const unsigned nb = more ? pbytes : 0u;
             const int d2 = more ? 2 : 0, d1 = more ? 1 : 0;
             const auto rA2 = prs(p.A, i + d2, nb);
@@ -404,7 +425,7 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WP
         }
 #pragma unroll
         for (int s = 0; s < RP; ++s) {
-            if (rg[s] == 1 || rg[s] == 2) {
+            if (W3D_TB3_ABL != 3 && (rg[s] == 1 || rg[s] == 2)) {
                 const T lap = lapA(H0, ry[s], rx[s], ra[s][S1], rxp[s], rxn[s]);
                 T cv;
                 if constexpr (DELTA) {
@@ -419,7 +440,7 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WP
             }
         }
         // C errors (own planes)
-        if (i >= ib && i <= ie) {
+        if (FAST || (i >= ib && i <= ie)) {
             errors(c[S0], i, p.ctC, ma1, mr1, chk1);
         }
         if constexpr (!ALIAS) {
@@ -439,7 +460,7 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WP
 
         // ---- D(i-1) on tile + 1-ring, from the C(i-1) tile --------------------------------
         const int id = i - 1;
-        if (id >= ib - 1 && id <= ie + 1) {
+        if (FAST || (id >= ib - 1 && id <= ie + 1)) {
 #pragma unroll
             for (int r = 0; r < R; ++r) {
                 const int y = 2 + w * R + r, x = 2 + lane;  // C tile coordinates
@@ -456,7 +477,7 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WP
             }
 #pragma unroll
             for (int s = 0; s < RP; ++s) {
-                if (rg[s] == 1) {
+                if (W3D_TB3_ABL != 3 && rg[s] == 1) {
                     const int y = ry[s] - 1, x = rx[s] - 1;
                     const T l = lap(1, rc[s][S3], rcp[s], rcn[s], ldsC[H1][y - 1][x], ldsC[H1][y + 1][x],
                                     ldsC[H1][y][x - 1], ldsC[H1][y][x + 1]);
@@ -466,7 +487,7 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WP
                         ldsD[H0][y - 1][x - 1] = rcd[s] ? leap(1, rc[s][S3], ra[s][S0], l) : T(0);
                 }
             }
-            if (id >= ib && id <= ie) {
+            if (FAST || (id >= ib && id <= ie)) {
                 if constexpr (!DELTA) {
                     const auto rd = prs(p.D, id, pbytes);
 #pragma unroll
@@ -487,7 +508,7 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WP
 
         // ---- E(i-2) on the tile, from the D(i-2) tile -----------------------------------------
         const int ie2 = i - 2;
-        if (ie2 >= ib && ie2 <= ie) {
+        if (FAST || (ie2 >= ib && ie2 <= ie)) {
             T ev[R];
 #pragma unroll
             for (int r = 0; r < R; ++r) {
@@ -534,7 +555,7 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WP
 
     auto step = [&](auto phase, const int i) {
         const bool seam = i == p.an_i || i == p.ap_i || i - 1 == p.an_i || i - 1 == p.ap_i;
-        if (seam) plane(phase, std::true_type{}, i);
+        if (seam || i < ib + 2 || i > ie) plane(phase, std::true_type{}, i);
         else plane(phase, std::false_type{}, i);
     };
 
