@@ -32,7 +32,7 @@
 #include "device_common.hpp"
 
 // timing ablations of the sweep (tools/ab_tb3_abl.sh builds; never the shipped library):
-// 1 = no error accumulation, 2 = errors without the analytic-table loads, 3 = no ring C/D
+// 1 = no error accumulation, 3 = no ring C/D
 #ifndef W3D_TB3_ABL
 #define W3D_TB3_ABL 0
 #endif
@@ -181,6 +181,24 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WP
         if (p.we_lo[g] <= ie && p.we_hi[g] >= ib) rare |= 2;
     }
     rare = __builtin_amdgcn_readfirstlane(rare);
+    // steady-state window [flo, fhi] of plane bodies: C(i), D(i-1), E(i-2) all own planes, off
+    // the periodic seam and the self-wrap planes. Those sit at the ends of the x range, so each
+    // one trims the window from its nearer end (a plane inside would only cost speed).
+    int flo = ib + 2, fhi = ie;
+    auto cut = [&](int lo, int hi) {
+        if (lo > hi || hi < flo || lo > fhi) return;
+        if (lo - flo <= fhi - hi) flo = hi + 1;
+        else fhi = lo - 1;
+    };
+    cut(p.an_i, p.an_i + 1);
+    cut(p.ap_i, p.ap_i + 1);
+#pragma unroll
+    for (int g = 0; g < 2; ++g) {
+        cut(p.wd_lo[g] + 1, p.wd_hi[g] + 1);
+        cut(p.we_lo[g] + 2, p.we_hi[g] + 2);
+    }
+    flo = __builtin_amdgcn_readfirstlane(flo);
+    fhi = __builtin_amdgcn_readfirstlane(fhi);
 
     // ---- ring positions of this thread ------------------------------------------------------
     // d-ring = rows jt-d / jt+TJ-1+d over cols kb-d+1 .. kb+64+d-2, then cols kb-d / kb+63+d over
@@ -284,17 +302,40 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WP
         if constexpr (FM) return FIRST ? ctr + l : leapfrog_fma(ctr, bv, l);
         else return FIRST ? taylor_first(ctr, l, p.coefC) : leapfrog(ctr, bv, l, p.coefC);
     };
-    // errors and finiteness sum of the own nodes of plane i of a layer (values v[r]); the
-    // uniform error-plane test sits outside the per-lane row masks (a scalar branch)
-    auto errors_exact = [&](const T(&v)[R], const int i, const T ct, T& ma, auto& mr, T& chk) {
-        if (i >= p.ei0 && i <= p.ei1) {
-            const T* const trow = txw + i * p.tpj;
+    // Errors are taken two planes late: at iteration i those of C(i-2), D(i-2) and E(i-2), all
+    // still in registers, so one analytic-table row per plane serves the three layers (f =
+    // ((sx sy) sz) ct per layer, as stencil_math analytic()). The row of plane i-1 is loaded at
+    // iteration i into the plane-parity slot (a scalar load a whole iteration ahead of its use).
+    // --math fma: the (sx sy, 1/|sx sy|) pair (txr); exact: sx sy (txy).
+    constexpr int NQ = FM ? 2 : 1;
+    T tq[2][R][NQ];
+    auto load_row = [&](int slot, int q) {
+        q = min(max(q, ib), ie);
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            if constexpr (FM) {
+                const T* const tr = p.txr + 2 * (q * p.tpj + (jt + w * R));
+                tq[slot][r][0] = ldconst(tr, 2 * r);
+                tq[slot][r][1] = ldconst(tr, 2 * r + 1);
+            } else {
+                tq[slot][r][0] = ldconst(txw + q * p.tpj, r);
+            }
+        }
+    };
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+#pragma unroll
+        for (int n = 0; n < NQ; ++n) tq[0][r][n] = tq[1][r][n] = T(0);
+    // exact: the reference's per-node error update (RelArg: bitwise relative error); the uniform
+    // error-plane test sits outside the per-lane row masks (a scalar branch)
+    auto errors_exact = [&](const T(&v)[R], const T(&fb)[R], const bool eplane, const T ct, T& ma, auto& mr,
+                            T& chk) {
+        if (eplane) {
 #pragma unroll
             for (int r = 0; r < R; ++r) {
                 if (!ovalid[r]) continue;
                 chk += v[r];
-                const T f = (ldconst(trow, r) * otz) * ct;  // = ((sx*sy)*sz)*ct, stencil_math analytic
-                accumulate_error_dev(v[r], f, ma, mr);
+                accumulate_error_dev(v[r], fb[r] * ct, ma, mr);
             }
         } else {
 #pragma unroll
@@ -302,35 +343,41 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WP
                 if (ovalid[r]) chk += v[r];
         }
     };
-
-    // --math fma: branch-free — every own plane, masked lanes and planes outside the error range
-    // contribute d = 0 (the multiplier om * em), so no exec-mask branches and no phi copies of the
-    // running maxima; one scalar load of the (sx sy, 1/|sx sy|) pair per row (txr table)
-    auto errors_fm = [&](const T(&v)[R], const int i, const T ct, T& ma, RelMax<T>& mr, T& chk) {
+    // --math fma: branch-free — masked lanes and planes outside the error range contribute
+    // d = 0 (the multiplier m = om * em), so no exec-mask branches and no phi copies of the
+    // running maxima; the relative weight wq = 1/|sx sy| * 1/|sz| is shared by the three layers
+    auto errors_fm = [&](const T(&v)[R], const T(&fb)[R], const T(&m)[R], const T(&wq)[R], const T ct, T& ma,
+                         RelMax<T>& mr, T& chk) {
 #if W3D_TB3_ABL == 1
         return;
 #endif
-        const T em = (i >= p.ei0 && i <= p.ei1) ? T(1) : T(0);
-        const T* const tr = p.txr + 2 * (i * p.tpj + (jt + w * R));
 #pragma unroll
         for (int r = 0; r < R; ++r) {
             chk += ovalid[r] ? v[r] : T(0);
-#if W3D_TB3_ABL == 2
-            const T f = (T(0.5) * otz) * ct;
-            const T dv = (v[r] - f) * (om[r] * em);
+            const T dv = (v[r] - fb[r] * ct) * m[r];
             ma = max_abs(ma, dv);
-            mr.add(dv, T(0.25) * ortz);
-#else
-            const T f = (ldconst(tr, 2 * r) * otz) * ct;  // = ((sx*sy)*sz)*ct
-            const T dv = (v[r] - f) * (om[r] * em);
-            ma = max_abs(ma, dv);
-            mr.add(dv, ldconst(tr, 2 * r + 1) * ortz);
-#endif
+            mr.add(dv, wq[r]);
         }
     };
-    auto errors = [&](const T(&v)[R], const int i, const T ct, T& ma, Rel& mr, T& chk) {
-        if constexpr (FM) errors_fm(v, i, ct, ma, mr, chk);
-        else errors_exact(v, i, ct, ma, mr, chk);
+    // the three layers of own plane q (table row in slot H)
+    auto errors3 = [&](const int H, const int q, const T(&vc)[R], const T(&vd)[R], const T(&ve)[R]) {
+        const bool eplane = q >= p.ei0 && q <= p.ei1;
+        T fb[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) fb[r] = tq[H][r][0] * otz;  // (sx sy) sz
+        if constexpr (FM) {
+            const T em = eplane ? T(1) : T(0);
+            T m[R], wq[R];
+#pragma unroll
+            for (int r = 0; r < R; ++r) m[r] = om[r] * em, wq[r] = tq[H][r][1] * ortz;
+            errors_fm(vc, fb, m, wq, p.ctC, ma1, mr1, chk1);
+            errors_fm(vd, fb, m, wq, p.ctD, ma2, mr2, chk2);
+            errors_fm(ve, fb, m, wq, p.ctE, ma3, mr3, chk3);
+        } else {
+            errors_exact(vc, fb, eplane, p.ctC, ma1, mr1, chk1);
+            errors_exact(vd, fb, eplane, p.ctD, ma2, mr2, chk2);
+            errors_exact(ve, fb, eplane, p.ctE, ma3, mr3, chk3);
+        }
     };
     // SLOW (ALIAS): the prologue / epilogue planes of the work item and the periodic seam
     // planes — every range check and the seam partners. FAST: the steady state (planes
@@ -439,10 +486,6 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WP
                 ldsC[H0][ry[s] - 1][rx[s] - 1] = cv;
             }
         }
-        // C errors (own planes)
-        if (FAST || (i >= ib && i <= ie)) {
-            errors(c[S0], i, p.ctC, ma1, mr1, chk1);
-        }
         if constexpr (!ALIAS) {
             // the x neighbours of D(i-1) are C(i) (computed just now) and C(i-2)
 #pragma unroll
@@ -492,7 +535,7 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WP
                     const auto rd = prs(p.D, id, pbytes);
 #pragma unroll
                     for (int r = 0; r < R; ++r) bst<2>(d[S0][r], rd, os[r]);
-                    if (rare & 1) {
+                    if (!FAST && (rare & 1)) {
 #pragma unroll
                         for (int g = 0; g < 2; ++g)
                             if (id >= p.wd_lo[g] && id <= p.wd_hi[g]) {
@@ -502,7 +545,6 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WP
                             }
                     }
                 }
-                errors(d[S0], id, p.ctD, ma2, mr2, chk2);
             }
         }
 
@@ -527,7 +569,7 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WP
                 const auto rd = prs(p.D, ie2, pbytes);
 #pragma unroll
                 for (int r = 0; r < R; ++r) bst<2>(dm1[H1][r], rd, os[r]);
-                if (rare & 2) {
+                if (!FAST && (rare & 2)) {
 #pragma unroll
                     for (int g = 0; g < 2; ++g)
                         if (ie2 >= p.we_lo[g] && ie2 <= p.we_hi[g]) {
@@ -540,7 +582,7 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WP
             const auto re = prs(p.E, ie2, pbytes);
 #pragma unroll
             for (int r = 0; r < R; ++r) bst<2>(ev[r], re, os[r]);
-            if (rare & 2) {
+            if (!FAST && (rare & 2)) {
 #pragma unroll
                 for (int g = 0; g < 2; ++g)
                     if (ie2 >= p.we_lo[g] && ie2 <= p.we_hi[g]) {
@@ -549,13 +591,14 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WP
                         for (int r = 0; r < R; ++r) bst<2>(ev[r], rw, os[r]);
                     }
             }
-            errors(ev, ie2, p.ctE, ma3, mr3, chk3);
+            // errors of plane i-2: C(i-2) and D(i-2) from their register slots, E(i-2) just now
+            errors3(H0, ie2, c[S2], d[S3], ev);
         }
+        load_row(H1, i - 1);
     };
 
     auto step = [&](auto phase, const int i) {
-        const bool seam = i == p.an_i || i == p.ap_i || i - 1 == p.an_i || i - 1 == p.ap_i;
-        if (seam || i < ib + 2 || i > ie) plane(phase, std::true_type{}, i);
+        if (i < flo || i > fhi) plane(phase, std::true_type{}, i);  // seam / wrap / ends
         else plane(phase, std::false_type{}, i);
     };
 
