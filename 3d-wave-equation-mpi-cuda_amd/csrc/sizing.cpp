@@ -37,14 +37,14 @@ Layout plan_layout(const Config& c, int world) {
     // 10.7 instead of 16 B per node-layer and beats tb2r2w8 by 12-14 % (leapfrog) / 3-4 %
     // (increment form), N=512 / 2048 (profiles/tb3_diet_r2.txt); fp64 stays on tb2
     // fp64 with --math fma: three-layer blocking too — the FMA form cuts the issue-bound fp64
-    // sweep's VALU work, and 1-row 8-wave tiles (124 VGPRs, 4 waves/SIMD) beat tb2r2w8 by
-    // 13-15 % (364k vs 316-323k Mpts/s at N=512, profiles/math_fma_r3.txt)
+    // sweep's VALU work (profiles/math_fma_r3.txt). After the scalar diet (steady-state body,
+    // errors of three layers per table row) the 16-row r2w8 tile (2 waves/SIMD) beats the
+    // 1-row r1w8 (4 waves/SIMD): 425-431k vs 402k Mpts/s at N=512 (profiles/tb3_salu_r3.txt)
     const bool auto_tb3 = auto_tb && (c.dtype == DType::F32 || c.fma);
     const bool tb3 = auto_tb3 || c.kernel.rfind("tb3", 0) == 0;
     l.tb = auto_tb || tb3 || c.kernel.rfind("tb2", 0) == 0;
     l.depth = tb3 ? 3 : (l.tb ? 2 : 1);
     if (tb3) l.rows = 2, l.waves = 8;  // measured best three-layer tile (profiles/)
-    if (auto_tb3 && c.dtype == DType::F64) l.rows = 1, l.waves = 8;
     // 16-row tiles of 8 waves (tb2r2w8, 2 workgroups per CU): fp64 +2-3 % over r2w4 (128
     // VGPRs, 4 waves/SIMD), fp32 +3.5 % (N=512) / +5 % (N=2048) over tb2r4 (profiles/
     // ab_tiles_r2.txt, fp32_accuracy_r2.txt). The fp64 increment form needs a few more

@@ -72,7 +72,7 @@ def test_bench_gpu_default_config_short():
     r = _bench(["--steps", "1", "--warmup", "1"])
     _check(r, 1, 1, 1)
     assert r["scaling"] == "weak" and r["config"]["N"] == 512 and r["config"]["timesteps"] == 100
-    assert r["math"] == "fma" and r["config"]["kernel"] == "tb3r1w8"  # the GPU default (presets)
+    assert r["math"] == "fma" and r["config"]["kernel"] == "tb3"  # the GPU default (presets)
     assert f"{r['linf_abs']:.6g}" == "6.03381e-07"  # golden N=512 K=100
     assert r["linf_golden"] == 6.03381e-07 and r["linf_ok"] is True
     assert r["config"]["dims"] == [1, 1, 1] and r["config"]["overlap"] is False  # no remote halo

@@ -10,7 +10,7 @@ run() {  # N ranks dims kernel math overlap
 }
 for cfg in "512 2 2,1,1" "1024 4 2,2,1" "1024 8 2,2,2"; do
   set -- $cfg
-  for km in "auto fma" "tb2r2w8 fma" "tb2r2w8 exact"; do
+  for km in ${KMS:-"auto fma" "tb2r2w8 fma" "tb2r2w8 exact"}; do
     for ov in on off; do
       echo -n "N=$1 ranks=$2 dims=$3 $km overlap=$ov: "
       run $1 $2 $3 $km $ov || exit 1
