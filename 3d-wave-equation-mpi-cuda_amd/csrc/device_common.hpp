@@ -5,7 +5,9 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <mutex>
 #include <type_traits>
+#include <unordered_map>
 
 #include "hip_kernels.hpp"
 #include "stencil_math.hpp"
@@ -221,6 +223,45 @@ inline int auto_chunk_boxes(int best, const int* tiles, const int* planes, int n
     }
     if (items >= kTarget) return best;
     return std::max(1, std::max(8, int(work / kTarget)));
+}
+
+// Resident workgroups of a sweep kernel on the whole device (CUs x occupancy), cached per kernel
+// and device (thread-per-GPU ranks launch concurrently).
+inline int resident_slots(const void* kern, int threads) {
+    static std::mutex mu;
+    static std::unordered_map<const void*, int> occ;
+    static int cus[64] = {};
+    int dev = 0;
+    HIP_OK(hipGetDevice(&dev));
+    std::lock_guard<std::mutex> lk(mu);
+    if (dev >= 0 && dev < 64 && cus[dev] == 0)
+        HIP_OK(hipDeviceGetAttribute(&cus[dev], hipDeviceAttributeMultiprocessorCount, dev));
+    auto it = occ.find(kern);
+    if (it == occ.end()) {
+        int n = 0;
+        HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, kern, threads, 0));
+        it = occ.emplace(kern, std::max(1, n)).first;
+    }
+    return std::max(1, (dev >= 0 && dev < 64 ? cus[dev] : 256) * it->second);
+}
+
+// Work-item length of a one-box sweep: the march pays `extra` planes of prologue/epilogue per
+// work item (tb3: 4, tb2: 2), and a launch runs in rounds of `slots` resident workgroups, so its
+// time goes as rounds x (chunk + extra). The 1-workgroup-per-CU fp64 tb3 sweep at N=512 (256 tiles): chunk 86
+// (the general auto_chunk) 430k, 171 450k, 256 453k, 512 449k Mpts/s (profiles/tb3_salu_r3.txt).
+// Takes the cheapest split; among splits within 1 % of it, the one with the most work items.
+inline int rounds_chunk(int planes, int tiles, int extra, int slots) {
+    auto cost = [&](int n) {
+        const int c = cdiv(planes, n), items = tiles * cdiv(planes, c);
+        return i64(cdiv(items, slots)) * (c + extra);
+    };
+    const int nmax = std::max(1, std::min(64, planes / 8));
+    i64 best = cost(1);
+    for (int n = 2; n <= nmax; ++n) best = std::min(best, cost(n));
+    int pick = 1;
+    for (int n = 1; n <= nmax; ++n)
+        if (cost(n) * 100 <= best * 101) pick = n;
+    return cdiv(planes, pick);
 }
 
 // ---- buffer addressing (T8): wave-uniform plane descriptor + 32-bit lane byte offset -----

@@ -655,7 +655,13 @@ void launch_tb2(int rows, int waves, int occ, int nwk, bool delta, bool fm, bool
         btiles[nbt] = ((bx.k1 - 1) / TK - (bx.k0 - 1) / TK + 1) * cdiv(bx.j1 - bx.j0 + 1, TJ) * nwk;
         bplanes[nbt++] = bx.i1 - bx.i0 + 1;
     }
-    const int achunk = auto_chunk_boxes(96, btiles, bplanes, nbt);
+    auto kern = fm ? (first ? tb_fma_kernel<T, true>(rows, waves, nwk, delta) : tb_fma_kernel<T, false>(rows, waves, nwk, delta))
+              : delta ? (first ? tb_delta_kernel<T, true>(rows, waves, nwk) : tb_delta_kernel<T, false>(rows, waves, nwk))
+                      : (first ? tb_kernel<T, true>(rows, waves, occ, nwk) : tb_kernel<T, false>(rows, waves, occ, nwk));
+    // one box: work items by resident-workgroup rounds (as launch_tb3); several: auto_chunk_boxes
+    const int achunk = nbt == 1 ? rounds_chunk(bplanes[0], btiles[0] / nwk, 2,
+                                               resident_slots(reinterpret_cast<const void*>(kern), waves * 64))
+                                : auto_chunk_boxes(96, btiles, bplanes, nbt);
     int nb = 0, total = 0;
     for (int q = 0; q < nbox; ++q) {
         const Box& bx = boxes[q];
@@ -678,9 +684,6 @@ void launch_tb2(int rows, int waves, int occ, int nwk, bool delta, bool fm, bool
     }
     p.nbox = nb;
     if (nb == 0) return;
-    auto kern = fm ? (first ? tb_fma_kernel<T, true>(rows, waves, nwk, delta) : tb_fma_kernel<T, false>(rows, waves, nwk, delta))
-              : delta ? (first ? tb_delta_kernel<T, true>(rows, waves, nwk) : tb_delta_kernel<T, false>(rows, waves, nwk))
-                      : (first ? tb_kernel<T, true>(rows, waves, occ, nwk) : tb_kernel<T, false>(rows, waves, occ, nwk));
     hipLaunchKernelGGL(kern, dim3(total), dim3(waves * 64), 0, s, p);
     HIP_OK(hipGetLastError());
 }

@@ -27,9 +27,7 @@
 #include <algorithm>
 #include <climits>
 #include <cmath>
-#include <mutex>
 #include <type_traits>
-#include <unordered_map>
 
 #include "device_common.hpp"
 
@@ -719,45 +717,6 @@ static void fma_coefs(const StepCoefs& c, T out[3]) {
     out[0] = T(c.coef / c.hx2), out[1] = T(c.coef / c.hy2), out[2] = T(c.coef / c.hz2);
 }
 
-// Resident workgroups of a sweep kernel on the whole device (CUs x occupancy), cached per kernel
-// and device (thread-per-GPU ranks launch concurrently).
-static int resident_slots(const void* kern, int threads) {
-    static std::mutex mu;
-    static std::unordered_map<const void*, int> occ;
-    static int cus[64] = {};
-    int dev = 0;
-    HIP_OK(hipGetDevice(&dev));
-    std::lock_guard<std::mutex> lk(mu);
-    if (dev >= 0 && dev < 64 && cus[dev] == 0)
-        HIP_OK(hipDeviceGetAttribute(&cus[dev], hipDeviceAttributeMultiprocessorCount, dev));
-    auto it = occ.find(kern);
-    if (it == occ.end()) {
-        int n = 0;
-        HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, kern, threads, 0));
-        it = occ.emplace(kern, std::max(1, n)).first;
-    }
-    return std::max(1, (dev >= 0 && dev < 64 ? cus[dev] : 256) * it->second);
-}
-
-// Work-item length of a one-box sweep: the march pays ~4 planes of prologue/epilogue per work
-// item, and a launch runs in rounds of `slots` resident workgroups, so its time goes as
-// rounds x (chunk + 4). The 1-workgroup-per-CU fp64 tb3 sweep at N=512 (256 tiles): chunk 86
-// (the general auto_chunk) 430k, 171 450k, 256 453k, 512 449k Mpts/s (profiles/tb3_salu_r3.txt).
-// Takes the cheapest split; among splits within 1 % of it, the one with the most work items.
-static int rounds_chunk(int planes, int tiles, int slots) {
-    auto cost = [&](int n) {
-        const int c = cdiv(planes, n), items = tiles * cdiv(planes, c);
-        return i64(cdiv(items, slots)) * (c + 4);
-    };
-    const int nmax = std::max(1, std::min(64, planes / 8));
-    i64 best = cost(1);
-    for (int n = 2; n <= nmax; ++n) best = std::min(best, cost(n));
-    int pick = 1;
-    for (int n = 1; n <= nmax; ++n)
-        if (cost(n) * 100 <= best * 101) pick = n;
-    return cdiv(planes, pick);
-}
-
 template <class T>
 void launch_tb3(int rows, int waves, bool delta, bool fm, bool first, const T* A, const T* B, T* D, T* E,
                 const GridView& gv, const Box* boxes, int nbox, const Box& cdom, int ei0, int ei1,
@@ -822,7 +781,7 @@ void launch_tb3(int rows, int waves, bool delta, bool fm, bool first, const T* A
         L.tiles_j = cdiv(bx.j1 - bx.j0 + 1, TJ);
         const int planes = bx.i1 - bx.i0 + 1;
         const int want = chunk > 0 ? std::min(chunk, planes)
-                         : live == 1 ? rounds_chunk(planes, L.tiles_k * L.tiles_j,
+                         : live == 1 ? rounds_chunk(planes, L.tiles_k * L.tiles_j, 4,
                                                     resident_slots(reinterpret_cast<const void*>(kern), waves * 64))
                                      : auto_chunk(96, planes, L.tiles_k * L.tiles_j);
         L.chunk = cdiv(planes, cdiv(planes, want));
