@@ -25,7 +25,7 @@ std::string usage() {
            "  --overlap auto|on|off  interior/shell split with the halo on a second stream; auto\n"
            "                         (default) times the first two solves on / off, keeps the faster\n"
            "  --no-overlap           = --overlap off\n"
-           "  --kernel K             auto (fp64: tb2r2w8, fp32: tb3) | tb2[r<R>][w<W>] | tb3[r<R>w<W>] | march[2|4|8][nt|p|f]\n"
+           "  --kernel K             auto (tb3; fp64 increment form: tb2r2w4) | tb2[r<R>][w<W>] | tb3[r<R>w<W>] | march[2|4|8][nt|p|f]\n"
            "                         | naive | flat   (temporal blocking / single-step variants)\n"
            "  --chunk C              i-planes per marching work item\n"
            "  --format new|omp|cuda|none      output file flavour (default new)\n"

@@ -40,7 +40,9 @@ Layout plan_layout(const Config& c, int world) {
     // sweep's VALU work (profiles/math_fma_r3.txt). After the scalar diet (steady-state body,
     // errors of three layers per table row) the 16-row r2w8 tile (2 waves/SIMD) beats the
     // 1-row r1w8 (4 waves/SIMD): 425-431k vs 402k Mpts/s at N=512 (profiles/tb3_salu_r3.txt)
-    const bool auto_tb3 = auto_tb && (c.dtype == DType::F32 || c.fma);
+    // fp64 exact leapfrog: tb3 too since the scalar diet — 373-374k vs tb2r2w8 317k Mpts/s at
+    // N=512, bitwise equal (profiles/tb3_salu_r3.txt); the fp64 increment form stays on tb2r2w4
+    const bool auto_tb3 = auto_tb && (c.dtype == DType::F32 || c.fma || !c.delta);
     const bool tb3 = auto_tb3 || c.kernel.rfind("tb3", 0) == 0;
     l.tb = auto_tb || tb3 || c.kernel.rfind("tb2", 0) == 0;
     l.depth = tb3 ? 3 : (l.tb ? 2 : 1);
