@@ -459,21 +459,28 @@ __global__ void k_encode(const double* v, u64* k, int n) {
 template <class T>
 struct BoxCopyOps {
     BoxCopy<T> op[kMaxBoxCopy];
+    unsigned first[kMaxBoxCopy + 1];  // first block of box q (blocks sized to each box)
+    int n;
 };
 
 template <class T>
 __global__ void __launch_bounds__(kThreads) k_box_copy(const BoxCopyOps<T> ops, i64 si, int sj,
                                                        bool to_buf) {
-    const BoxCopy<T> o = ops.op[blockIdx.y];
-    const int nk = o.b.k1 - o.b.k0 + 1, nj = o.b.j1 - o.b.j0 + 1;
-    const i64 total = i64(o.b.i1 - o.b.i0 + 1) * nj * nk;
-    for (i64 e = i64(blockIdx.x) * blockDim.x + threadIdx.x; e < total;
-         e += i64(gridDim.x) * blockDim.x) {
-        const int k = o.b.k0 + int(e % nk);
-        const i64 r = e / nk;
-        const int j = o.b.j0 + int(r % nj);
-        const int i = o.b.i0 + int(r / nj);
-        T* g = o.grid + i64(i) * si + i64(j) * sj + k;
+    // one 1-D grid over every box, each box getting the blocks its size needs (a launch carries
+    // a peer's faces, edges and corners: blocks sized to the largest box left most idle)
+    int q = 0;
+    for (int t = 1; t < ops.n; ++t)
+        if (blockIdx.x >= ops.first[t]) q = t;
+    const BoxCopy<T> o = ops.op[q];
+    const unsigned b0 = ops.first[q], nb = ops.first[q + 1] - b0;
+    // 32-bit element indices (the host checks the box size): unsigned 32-bit div/mod by the
+    // wave-uniform extents are a few VALU each, the 64-bit ones a long subroutine per element
+    const unsigned nk = unsigned(o.b.k1 - o.b.k0 + 1), nj = unsigned(o.b.j1 - o.b.j0 + 1);
+    const unsigned total = unsigned(o.b.i1 - o.b.i0 + 1) * nj * nk;
+    for (unsigned e = (blockIdx.x - b0) * blockDim.x + threadIdx.x; e < total; e += nb * blockDim.x) {
+        const unsigned r = e / nk, k = e - r * nk;
+        const unsigned ii = r / nj, j = r - ii * nj;
+        T* g = o.grid + i64(o.b.i0 + int(ii)) * si + i64(o.b.j0 + int(j)) * sj + (o.b.k0 + int(k));
         if (to_buf) o.buf[e] = *g;
         else *g = o.buf[e];
     }
@@ -797,18 +804,21 @@ void launch_box_copy(const BoxCopy<T>* ops, int nops, const GridView& gv, bool t
     W3D_REQUIRE(nops >= 0 && nops <= kMaxBoxCopy, "too many halo boxes in one launch");
     if (nops == 0) return;
     BoxCopyOps<T> p{};
-    i64 most = 0;
+    p.n = nops;
+    unsigned blocks = 0;
     for (int q = 0; q < nops; ++q) {
         const Box& b = ops[q].b;
         W3D_REQUIRE(!b.empty() && b.i0 >= 1 - gv.G && b.i1 <= gv.X + gv.G && b.j0 >= 1 - gv.G &&
                         b.j1 <= gv.Y + gv.G && b.k0 >= 1 - gv.G && b.k1 <= gv.Z + gv.G,
                     "halo box outside the storage");
         p.op[q] = ops[q];
-        most = std::max(most, i64(b.i1 - b.i0 + 1) * (b.j1 - b.j0 + 1) * (b.k1 - b.k0 + 1));
+        const i64 n = i64(b.i1 - b.i0 + 1) * (b.j1 - b.j0 + 1) * (b.k1 - b.k0 + 1);
+        W3D_REQUIRE(n < (i64(1) << 31), "halo box larger than 2^31 elements");
+        p.first[q] = blocks;
+        blocks += unsigned(std::min<i64>(2048, (n + kThreads - 1) / kThreads));
     }
-    const int blocks = int(std::min<i64>(2048, (most + kThreads - 1) / kThreads));
-    hipLaunchKernelGGL(k_box_copy<T>, dim3(blocks, nops), dim3(kThreads), 0, s, p, gv.si, gv.sj,
-                       to_buf);
+    p.first[nops] = blocks;
+    hipLaunchKernelGGL(k_box_copy<T>, dim3(blocks), dim3(kThreads), 0, s, p, gv.si, gv.sj, to_buf);
     HIP_OK(hipGetLastError());
 }
 template void launch_box_copy<double>(const BoxCopy<double>*, int, const GridView&, bool, hipStream_t);

@@ -2,7 +2,7 @@
 # Simulated multi-rank bench configs (one GPU, loopback halos) for a list of fp64 fma kernels,
 # overlap off: tools/r3_mr_tiles.sh tb3r1w8 tb3 ...
 cd "$(dirname "$0")/.."
-B=3d-wave-equation-mpi-cuda_amd/build/wave3d
+B=${BIN:-3d-wave-equation-mpi-cuda_amd/build/wave3d}
 for k in "$@"; do
   for cfg in 512:2:2,1,1 1024:4:2,2,1 1024:8:2,2,2; do
     IFS=: read n r d <<< "$cfg"
