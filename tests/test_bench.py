@@ -65,6 +65,7 @@ def test_bench_cpu_two_ranks_gloo():
     _check(r, 2, 1, 0)
     assert r["scaling"] == "strong"  # global N fixed by --N
     assert f"{r['linf_abs']:.6g}" == "0.000175963"
+    assert r["tuning_solves"] == 0  # no overlap trials on the CPU backend
 
 
 @pytest.mark.gpu
@@ -107,6 +108,7 @@ def test_bench_gpu_multirank_plan_staged(n, N, dims, golden):
     assert r["config"]["timesteps"] == 100 and r["linf_golden"] == golden and r["linf_ok"] is True
     assert r["halo_checked"] > 0 and r["value"] > 0
     assert r["config"]["overlap_mode"] == "auto" and min(r["config"]["overlap_trial_ms"]) > 0
+    assert r["warmup"] == 2 and r["tuning_solves"] == 1  # the second trial solve ran untimed
     assert r["timers_ms"]["exchange_ms"] > 0 and r["timers_ms"]["comm_ms"] > 0
 
 
@@ -168,6 +170,7 @@ def test_bench_gpu_self_launch_two_ranks_staged():
     r = _bench(["--steps", "1", "--warmup", "0", "--transport", "staged", "--shared-device"], nproc=2,
                timeout=600, self_launch=True)
     _check(r, 2, 1, 0)
+    assert r["tuning_solves"] == 3  # overlap auto: warm-up + both trials before the timed solve
     assert r["launch"] == "self" and r["config"]["N"] == 512 and r["config"]["dims"] == [2, 1, 1]
     assert r["config"]["timesteps"] == 100 and r["linf_ok"] is True
     assert r["halo_checked"] > 0
