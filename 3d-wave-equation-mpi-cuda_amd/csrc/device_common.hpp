@@ -264,6 +264,31 @@ inline int rounds_chunk(int planes, int tiles, int extra, int slots) {
     return cdiv(planes, pick);
 }
 
+// The same for a launch over several boxes (overlap shells: thin x slabs, one tile band in j
+// and k): one chunk c for every box (each box's items cut to min(c, planes)); the launch takes
+// about max(longest item, total item-planes / slots), items costing planes + `extra` each.
+inline int rounds_chunk_boxes(const int* tiles, const int* planes, int n, int extra, int slots) {
+    int pmax = 1;
+    for (int q = 0; q < n; ++q) pmax = std::max(pmax, planes[q]);
+    auto cost = [&](int c) {
+        i64 work = 0;
+        int longest = 0;
+        for (int q = 0; q < n; ++q) {
+            const int cq = cdiv(planes[q], cdiv(planes[q], std::min(c, planes[q])));
+            work += i64(tiles[q]) * cdiv(planes[q], cq) * (cq + extra);
+            longest = std::max(longest, cq + extra);
+        }
+        return std::max<i64>(longest * i64(slots), work);  // in plane-iterations x slots
+    };
+    int best_c = pmax;
+    i64 best = cost(pmax);
+    for (int c = 8; c < pmax; c += (c < 64 ? 8 : 16)) {
+        const i64 v = cost(c);
+        if (v < best) best = v, best_c = c;
+    }
+    return best_c;
+}
+
 // ---- buffer addressing (T8): wave-uniform plane descriptor + 32-bit lane byte offset -----
 // An offset >= the descriptor's byte size is out of range: loads return 0, stores are
 // dropped — masked lanes use kOOB instead of a branch around the access.

@@ -766,6 +766,18 @@ void launch_tb3(int rows, int waves, bool delta, bool fm, bool first, const T* A
                       : (first ? tb3_kernel<T, true>(rows, waves, fm) : tb3_kernel<T, false>(rows, waves, fm));
     int live = 0;
     for (int q = 0; q < nbox; ++q) live += !boxes[q].empty();
+    // several boxes (overlap shells): one work-item length for the launch as a whole
+    int multi_chunk = 0;
+    if (chunk <= 0 && live > 1) {
+        int bt[kMaxBoxes], bp[kMaxBoxes], m = 0;
+        for (int q = 0; q < nbox; ++q) {
+            const Box& bx = boxes[q];
+            if (bx.empty()) continue;
+            bt[m] = ((bx.k1 - 1) / kTK - (bx.k0 - 1) / kTK + 1) * cdiv(bx.j1 - bx.j0 + 1, TJ);
+            bp[m++] = bx.i1 - bx.i0 + 1;
+        }
+        multi_chunk = rounds_chunk_boxes(bt, bp, m, 4, resident_slots(reinterpret_cast<const void*>(kern), waves * 64));
+    }
     int nb = 0, total = 0;
     for (int q = 0; q < nbox; ++q) {
         const Box& bx = boxes[q];
@@ -783,7 +795,7 @@ void launch_tb3(int rows, int waves, bool delta, bool fm, bool first, const T* A
         const int want = chunk > 0 ? std::min(chunk, planes)
                          : live == 1 ? rounds_chunk(planes, L.tiles_k * L.tiles_j, 4,
                                                     resident_slots(reinterpret_cast<const void*>(kern), waves * 64))
-                                     : auto_chunk(96, planes, L.tiles_k * L.tiles_j);
+                                     : std::min(multi_chunk, planes);
         L.chunk = cdiv(planes, cdiv(planes, want));
         L.block_begin = total;
         total += L.tiles_k * L.tiles_j * cdiv(planes, L.chunk);
