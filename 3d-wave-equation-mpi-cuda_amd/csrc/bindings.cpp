@@ -6,6 +6,8 @@
 //   Transport                      subclassable from Python (e.g. torch.distributed/gloo)
 //   k_* functions                  the individual HIP kernels, for numerics tests
 #include <hip/hip_runtime.h>
+#include <algorithm>
+
 #include <pybind11/functional.h>
 #include <pybind11/pybind11.h>
 
@@ -97,7 +99,10 @@ py::dict result_dict(const Config& c, const RunResult& r) {
     d["overlap"] = r.overlap;
     d["overlap_mode"] = r.overlap_mode;
     d["overlap_trial_ms"] = py::make_tuple(r.overlap_trial_ms[0], r.overlap_trial_ms[1]);
+    d["overlap_trials_ms"] =
+        py::make_tuple(r.overlap_trials[0], r.overlap_trials[1], r.overlap_trials[2], r.overlap_trials[3]);
     d["comm_size"] = r.comm_size;
+    d["rccl_max_ctas"] = r.rccl_max_ctas;
     d["halo_checked"] = r.halo_checked;
     d["overlap_interior"] = r.overlap_interior;
     d["rccl_mirror_msgs"] = r.rccl_mirror_msgs;
@@ -107,9 +112,17 @@ py::dict result_dict(const Config& c, const RunResult& r) {
     return d;
 }
 
+// The in-process API is quiet by default: the programs' per-layer progress lines
+// ("calculating layer n", cuda_sol.cpp:385) only with an explicit --print-layers.
+Config parse_api(const std::vector<std::string>& args) {
+    Config c = parse_cli(args);
+    if (std::find(args.begin(), args.end(), "--print-layers") == args.end()) c.print_layers = false;
+    return c;
+}
+
 py::dict run(const std::vector<std::string>& args, const std::string& backend,
              Transport* transport, bool write, bool root) {
-    Config c = parse_cli(args);
+    Config c = parse_api(args);
     RunResult r;
     {
         py::gil_scoped_release nogil;
@@ -308,12 +321,13 @@ PYBIND11_MODULE(_wave3d_C, m) {
         .def("device", &Transport::device);
 
     py::class_<RcclTransport, Transport>(m, "RcclTransport")
-        .def(py::init([](int rank, int size, py::bytes uid, int device) {
+        .def(py::init([](int rank, int size, py::bytes uid, int device, int max_ctas) {
                  std::string s = uid;
                  py::gil_scoped_release nogil;
-                 return new RcclTransport(rank, size, s, device);
+                 return new RcclTransport(rank, size, s, device, max_ctas);
              }),
-             py::arg("rank"), py::arg("size"), py::arg("uid"), py::arg("device"))
+             py::arg("rank"), py::arg("size"), py::arg("uid"), py::arg("device"), py::arg("max_ctas") = -1)
+        .def("max_ctas", &RcclTransport::max_ctas)
         .def("barrier", [](RcclTransport& t) {
             py::gil_scoped_release nogil;
             t.barrier();
@@ -321,11 +335,13 @@ PYBIND11_MODULE(_wave3d_C, m) {
         .def("check_async", &RcclTransport::check_async)
         .def("comm_size", &RcclTransport::comm_size);
     m.def("rccl_unique_id", []() { return py::bytes(rccl_unique_id()); });
+    m.def("rccl_max_ctas", &rccl_max_ctas, py::arg("overlap_mode") = "auto",
+          "CTA budget a halo communicator gets for an overlap mode (WAVE3D_RCCL_MAX_CTAS overrides)");
 
     py::class_<Session>(m, "Session", "Persistent solver: allocate once, solve() many times")
         .def(py::init([](const std::vector<std::string>& args, const std::string& backend,
                          Transport* tr) {
-                 Config c = parse_cli(args);
+                 Config c = parse_api(args);
                  py::gil_scoped_release nogil;
                  if (backend == "cpu") return make_cpu_session(c, tr).release();
                  if (backend == "hip") return make_hip_session(c, tr).release();

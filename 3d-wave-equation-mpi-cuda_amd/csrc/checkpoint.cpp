@@ -35,6 +35,7 @@ CheckpointHeader make_header(const Config& c, const Topology& t, int layer, int 
     h.Ly = c.Ly_is_pi ? -1.0 : c.Ly;
     h.Lz = c.Lz_is_pi ? -1.0 : c.Lz;
     h.scheme = c.delta ? 1 : 0;
+    h.math = c.fma ? 1 : 0;
     return h;
 }
 
@@ -117,7 +118,7 @@ bool same_run(const CheckpointHeader& h, const CheckpointHeader& e) {
     bool same = std::memcmp(h.magic, e.magic, 8) == 0 && h.N == e.N && h.K == e.K && h.nprocs == e.nprocs &&
                 h.rank == e.rank && h.elem_size == e.elem_size && h.pi_mode == e.pi_mode &&
                 h.ic_mode == e.ic_mode && h.T == e.T && h.Lx == e.Lx && h.Ly == e.Ly && h.Lz == e.Lz &&
-                h.scheme == e.scheme;
+                h.scheme == e.scheme && h.math == e.math;
     for (int a = 0; a < 3; ++a)
         same = same && h.dims[a] == e.dims[a] && h.coords[a] == e.coords[a] && h.ext[a] == e.ext[a];
     return same;

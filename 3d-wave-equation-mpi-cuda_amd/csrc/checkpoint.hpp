@@ -23,7 +23,7 @@
 namespace wave3d {
 
 struct CheckpointHeader {
-    char magic[8] = {'W', '3', 'D', 'C', 'K', 'P', 'T', '2'};
+    char magic[8] = {'W', '3', 'D', 'C', 'K', 'P', 'T', '3'};  // 3: + math (files of version 2 are refused)
     int N = 0, K = 0, nprocs = 0, rank = 0;
     int dims[3] = {0, 0, 0};
     int coords[3] = {0, 0, 0};
@@ -33,12 +33,13 @@ struct CheckpointHeader {
     int pi_mode = 0, ic_mode = 0;
     double T = 0, Lx = 0, Ly = 0, Lz = 0;
     int scheme = 0;  // 0 leapfrog: levels u^{n-1}, u^n; 1 increment form: d^n, u^n
-    int pad = 0;
+    int math = 0;    // 0 exact (bitwise with the reference programs), 1 --math fma
 };
 
 CheckpointHeader make_header(const Config& c, const Topology& t, int layer, int elem_size);
 std::string checkpoint_path(const std::string& dir, int rank, int layer);
-// Same run: every header field but the layer (N, K, decomposition, physics, dtype, scheme).
+// Same run: every header field but the layer (N, K, decomposition, physics, dtype, scheme,
+// arithmetic: an fma run never resumes from — or prunes — an exact run's files, or the reverse).
 bool same_run(const CheckpointHeader& a, const CheckpointHeader& b);
 // Layers for which `rank` has a complete checkpoint file in `dir`, ascending; with `match`,
 // only files written by the same run configuration (a directory may hold files of others).

@@ -81,4 +81,7 @@ Config parse_cli(const std::vector<std::string>& args);  // args without argv[0]
 
 std::string usage();
 
+// "on" | "off" | "auto" — the run's --overlap mode (sizes the RCCL CTA budget)
+inline std::string overlap_mode(const Config& c) { return !c.overlap ? "off" : (c.overlap_auto ? "auto" : "on"); }
+
 }  // namespace wave3d

@@ -87,6 +87,9 @@ public:
     // Ranks of the underlying communicator as the library itself reports them (RCCL:
     // ncclCommCount), so a run can prove which world the halos travelled in.
     virtual int comm_size() const { return size(); }
+    // CTA budget of a GPU collective library's communicator (RCCL maxCTAs; 0 = the library's
+    // own), -1 when the transport has none
+    virtual int cta_budget() const { return -1; }
     virtual void exchange(const std::vector<Message>& sends, const std::vector<Message>& recvs,
                           void* stream) = 0;
     // In-place max over ranks of n order-preserving error keys (see encode_max_key).

@@ -54,7 +54,7 @@ std::string tb_name(int rows, int waves, int occ, int depth = 2, int kwaves = 1)
     return s;
 }
 
-constexpr int kMaxLevels = 5;  // time levels: 3 single-step, 4 tb2, 5 tb3
+constexpr int kMaxLevels = 4;  // time levels: 3 single-step, 4 with two- / three-layer sweeps
 
 template <class T>
 struct DevRank {
@@ -196,6 +196,7 @@ public:
         TraceRange tr("wave3d.setup");
         auto t0 = clk::now();
         setup();
+        plan_slots(1);
         if (cfg_.rccl_mirror) setup_mirror();
         bool msgs = false;
         for (auto& R : ranks_) msgs |= !R.plan.sends.empty() || !R.plan.recvs.empty() || tb_halo(R);
@@ -248,13 +249,14 @@ public:
         res.kernel = tb_ ? tb_name(tb_rows_, tb_waves_, tb_occ_, tbd_, tb_nwk_) : kernel_variant_name(kind_);
         res.courant = prob_.courant;
         res.transport = ext_ ? ext_->name() : (world_ > 1 ? "loopback" : "self");
-        // --overlap auto: solves 2 and 3 are the trials (on, then off; the first solve only warms
+        // --overlap auto: solves 2..5 are the trials (on, off, on, off; the first solve only warms
         // up — first launches, RCCL connections of every message shape); the arm with the
-        // shorter max-over-ranks solve time is kept for every later solve — the same decision on
-        // every rank, since the times are reduced before the comparison
-        const int trial = overlap_auto_ && solves_ >= 1 && trials_done_ < 2 ? trials_done_ : -1;
+        // shorter best-of-two max-over-ranks solve time is kept for every later solve (one noisy
+        // sample cannot lock in the slower arm) — the same decision on every rank, since the
+        // times are reduced before the comparison
+        const int trial = overlap_auto_ && solves_ >= 1 && trials_done_ < kOverlapTrials ? trials_done_ : -1;
         ++solves_;
-        if (trial >= 0) set_overlap(trial == 0);
+        if (trial >= 0) set_overlap(trial % 2 == 0);
         res.overlap = overlap_;
         res.overlap_mode = !(ext_ || world_ > 1) ? "none"
                            : overlap_auto_       ? "auto"
@@ -262,6 +264,7 @@ public:
         res.scheme = cfg_.delta ? "delta" : "leapfrog";
         res.math = cfg_.fma ? "fma" : "exact";
         res.comm_size = ext_ ? ext_->comm_size() : 0;
+        res.rccl_max_ctas = ext_ ? ext_->cta_budget() : -1;
         res.halo_checked = halo_checked_;
         if (ext_ || world_ > 1) {
             res.overlap_interior = -1;
@@ -280,13 +283,14 @@ public:
         t.error_ms = tv[4];
         if (trial >= 0) {
             trial_ms_[trial] = t.total_ms;
-            if (++trials_done_ == 2) {
-                set_overlap(trial_ms_[0] <= trial_ms_[1]);
-                log_msg(LogLevel::Info, "overlap auto: on ", trial_ms_[0], " ms, off ", trial_ms_[1], " ms -> ",
-                        overlap_ ? "on" : "off");
+            if (++trials_done_ == kOverlapTrials) {
+                set_overlap(best_trial(0) <= best_trial(1));
+                log_msg(LogLevel::Info, "overlap auto: on ", trial_ms_[0], "/", trial_ms_[2], " ms, off ", trial_ms_[1],
+                        "/", trial_ms_[3], " ms -> ", overlap_ ? "on" : "off");
             }
         }
-        res.overlap_trial_ms[0] = trial_ms_[0], res.overlap_trial_ms[1] = trial_ms_[1];
+        res.overlap_trial_ms[0] = best_trial(0), res.overlap_trial_ms[1] = best_trial(1);
+        for (int q = 0; q < kOverlapTrials; ++q) res.overlap_trials[q] = trial_ms_[q];
         res.t = t;
         res.solve_ms.push_back(t.total_ms);
         return res;
@@ -537,7 +541,49 @@ private:
     T* plane(DevRank<T>& R, int level, int i) {
         return R.g[level] + i64(i) * R.gv.si - R.plane_off;
     }
-    int lvl(int n) const { return n % L_; }
+    // Level buffer of layer n (n = -1 .. K): slot_[n + 1], planned by plan_slots() from the
+    // run's own schedule of sweeps. Each sweep reads the two newest stored layers and writes
+    // its stored layers into the other slots, so L_ = 4 buffers serve every schedule with up
+    // to two stored layers per operation — three-layer sweeps included (their C = u^m is never
+    // stored), where a `n % L` ring needed 5 (the slot of u^m sat idle). The reference keeps 3
+    // rolling levels (mpi_new.cpp:458-460) for one stored layer per step.
+    int lvl(int n) const {
+        W3D_REQUIRE(n >= -1 && size_t(n + 1) < slot_.size(), "level of a layer outside the planned schedule");
+        return slot_[n + 1];
+    }
+    // layers computed by the operation that starts at layer n (3: three-layer sweep, 2: two-
+    // layer sweep, 1: single step) — the schedule of enqueue_layers()
+    int span_at(int n) const { return (tbd_ == 3 && n + 2 <= prob_.K) ? 3 : ((tb_ && n + 1 <= prob_.K) ? 2 : 1); }
+    // Slot plan of a solve that starts at layer `start` (1, or the layer after a resumed
+    // checkpoint): layers start-1 / start-2 in slots 0 / 1; every operation then takes the
+    // lowest free slots for the layers it stores. A three-layer sweep's C layer maps to the slot
+    // of its E layer (n + 2), so lookups of it (checkpoint guards) name a level the sweep writes.
+    // first_write_[n + 1]: layer n is the first of this solve written into its slot.
+    void plan_slots(int start) {
+        const int K = prob_.K;
+        slot_.assign(size_t(K) + 2, 0);
+        first_write_.assign(size_t(K) + 2, 0);
+        W3D_REQUIRE(start >= 1 && start <= K + 1, "bad first layer");
+        slot_[start] = 0;       // layer start - 1
+        slot_[start - 1] = 1;   // layer start - 2
+        std::vector<char> used(size_t(L_), 0);
+        for (int n = start; n <= K;) {
+            const int span = span_at(n);
+            const int live[2] = {slot_[n], slot_[n - 1]};  // layers n - 1, n - 2
+            const int first_stored = span == 3 ? n + 1 : n;
+            int l = 0;
+            for (int q = first_stored; q < n + span; ++q) {
+                while (l == live[0] || l == live[1]) ++l;
+                W3D_REQUIRE(l < L_, "level plan needs more time levels than allocated");
+                slot_[q + 1] = l;
+                first_write_[q + 1] = !used[l];
+                used[l] = 1;
+                ++l;
+            }
+            if (span == 3) slot_[n + 1] = slot_[n + 3];
+            n += span;
+        }
+    }
     const Wrap& wrap_depth(const DevRank<T>& R, int d) const {
         return d >= 3 ? R.wrap3 : (d == 2 ? R.wrap2 : R.wrap);
     }
@@ -569,8 +615,8 @@ private:
 
     void step_boxes(DevRank<T>& R, int n, const Box* boxes, int nbox, const KernelVariant& kind,
                     hipStream_t s) {
-        const T* u1 = R.g[lvl(n + L_ - 1)];
-        const T* u2 = R.g[lvl(n + L_ - 2)];
+        const T* u1 = R.g[lvl(n - 1)];
+        const T* u2 = R.g[lvl(n - 2)];
         launch_step<T>(kind, n == 1, u1, u2, R.g[lvl(n)], R.gv, boxes, nbox, R.error.i0,
                        R.error.i1, R.wrap, R.pack, R.tx, R.ty, R.tz, coefs(n),
                        R.err + size_t(n) * kSlotsPerLayer, cfg_.chunk, s);
@@ -835,7 +881,7 @@ private:
 
     void* tb_ptr(DevRank<T>& R, const typename DevRank<T>::PlaneMsg& m, int mD) {
         if (m.plane == kAliasPlane) return m.level == 0 ? R.alias_buf : R.alias_bufB;
-        return plane(R, lvl(m.level == 0 ? mD : mD - 1 + L_), m.plane);
+        return plane(R, lvl(m.level == 0 ? mD : mD - 1), m.plane);
     }
 
     // exchange after a sweep whose D layer is mD (A level = mD, B level = mD-1)
@@ -846,7 +892,7 @@ private:
     T* direct_grid(DevRank<T>& R, int level, int mD, bool send) {
         if (level == 2 && !send) return R.alias_buf + R.plane_off;
         if (level == 3 && !send) return R.alias_bufB + R.plane_off;
-        return R.g[lvl(level % 2 == 0 ? mD : mD - 1 + L_)];
+        return R.g[lvl(level % 2 == 0 ? mD : mD - 1)];
     }
     void box_copies(DevRank<T>& R, std::vector<typename DevRank<T>::BoxMsg>& v, int mD, bool to_buf, hipStream_t s) {
         for (size_t q0 = 0; q0 < v.size(); q0 += kMaxBoxCopy) {
@@ -961,7 +1007,7 @@ private:
                     BoxCopy<T> b;
                     // level 2 = the seam alias plane (a one-plane buffer at logical i = 0)
                     b.grid = m.level == 2 ? R.alias_buf + R.plane_off
-                                          : R.g[lvl(m.level == 0 ? mD : mD - 1 + L_)];
+                                          : R.g[lvl(m.level == 0 ? mD : mD - 1)];
                     b.buf = m.buf;
                     b.b = m.box;
                     o.push_back(b);
@@ -1010,8 +1056,8 @@ private:
 
     // temporal-blocking sweep: layers m (C) and m+1 (D) from m-1 (A) and m-2 (B)
     void sweep(DevRank<T>& R, int m, hipStream_t s, const Box* boxes = nullptr, int nbox = 0) {
-        const T* A = R.g[lvl(m + L_ - 1)];
-        const T* B = R.g[lvl(m + L_ - 2)];
+        const T* A = R.g[lvl(m - 1)];
+        const T* B = R.g[lvl(m - 2)];
         SeamAlias<T> al;
         if (R.topo.dims[0] == 1) {  // self-wrap, fused or through the transport
             al.next_i = 0;  // ghost copy of N-1 sees x=N (own plane X) as its x+ neighbour
@@ -1040,8 +1086,8 @@ private:
 
     // Three-layer sweep m: C = u^m (registers only), D = u^{m+1}, E = u^{m+2}.
     SeamPartners<T> seam_partners(DevRank<T>& R, int m, std::vector<SeamCPlane<T>>* ops) {
-        const T* A = R.g[lvl(m + L_ - 1)];
-        const T* B = R.g[lvl(m + L_ - 2)];
+        const T* A = R.g[lvl(m - 1)];
+        const T* B = R.g[lvl(m - 2)];
         const i64 si = R.gv.si;
         const int X = R.topo.X();
         SeamPartners<T> sp;
@@ -1079,8 +1125,8 @@ private:
     }
 
     void sweep3(DevRank<T>& R, int m, hipStream_t s, const Box* boxes = nullptr, int nbox = 0) {
-        const T* A = R.g[lvl(m + L_ - 1)];
-        const T* B = R.g[lvl(m + L_ - 2)];
+        const T* A = R.g[lvl(m - 1)];
+        const T* B = R.g[lvl(m - 2)];
         const SeamPartners<T> sp = seam_partners(R, m, nullptr);
         if (!boxes) boxes = &R.compute, nbox = 1;
         launch_tb3<T>(tb_rows_, tb_waves_, cfg_.delta, cfg_.fma, m == 1, A, B, R.g[lvl(m + 1)], R.g[lvl(m + 2)], R.gv, boxes,
@@ -1324,7 +1370,10 @@ private:
         TraceRange tr("wave3d.halo_selftest");
         const bool deep = tb_ && tb_halo(ranks_[0]);
         const int mD = 2;  // deep: A level = lvl(2), B = lvl(1) (as exchange_tb); faces: lvl(1)
-        const int lA = deep ? lvl(mD) : lvl(1), lB = lvl(mD - 1 + L_);
+        // a fixed slot plan for the test (layers -1..2 -> slots 2, 3, 1, 0), independent of K
+        const std::vector<int> run_slots = slot_;
+        slot_ = {2, 3, 1, 0};
+        const int lA = deep ? lvl(mD) : lvl(1), lB = lvl(mD - 1);
         const unsigned sA = 0xA11CEu, sB = 0xB0B5u;
         hipStream_t s = s_comp_;
         std::vector<std::vector<CheckRegion>> regs;
@@ -1409,6 +1458,7 @@ private:
             if (R.alias_bufB) HIP_CHECK(hipMemsetAsync(R.alias_bufB, 0, R.gv.si * sizeof(T), s));
         }
         sync(s);
+        slot_ = run_slots;
         if (v > 0)
             throw Error("wave3d: halo self-test failed" +
                         (report.empty() ? std::string(" on another rank (this rank's messages were correct)")
@@ -1464,13 +1514,12 @@ private:
 
         res.resumed_from = -1;
         res.aborted = false;
+        plan_slots(1);  // a resume re-plans from its checkpoint layer (load_checkpoints)
         if (graph_eligible() && !gexec_ && !graph_failed_) build_graph(res);  // host-only work
         HIP_CHECK(hipEventRecord(ev_start_, s_comp_));
         if (gexec_) {
             // the whole IC + time loop as one graph launch (no per-kernel host overhead); its
             // timer marks were captured with it
-            if (cfg_.print_layers && !cfg_.quiet && ranks_[0].topo.rank == 0)
-                for (int q = 1; q <= K; ++q) std::cout << "calculating layer " << q << "\n";
             tn_ = graph_tn_;
             stamped_ = true;
             HIP_CHECK(hipGraphLaunch(gexec_, s_comp_));
@@ -1509,6 +1558,9 @@ private:
         HIP_CHECK(hipEventRecord(ev_end_, s_comp_));
         if (mirror_) check_mirror(ranks_[0].err, nslot, s_comp_);  // outside the timed interval
         HIP_CHECK(hipEventSynchronize(ev_end_));
+        // graph replay: the progress lines once the layers are done (one launch runs them all)
+        if (res.graph && cfg_.print_layers && !cfg_.quiet && ranks_[0].topo.rank == 0)
+            for (int q = 1; q <= K; ++q) std::cout << "calculating layer " << q << "\n";
         finish_checkpoint();  // files complete when solve() returns
         float ms = 0;
         HIP_CHECK(hipEventElapsedTime(&ms, ev_start_, ev_end_));
@@ -1531,7 +1583,7 @@ private:
         TraceRange tr("wave3d.ic");
         mark(s_comp_, 0, kAlways);
         for (auto& R : ranks_) {
-            launch_init<T>(R.g[0], R.gv, R.owned, wrap_depth(R, G_), R.tx, R.ty, R.tz, ct_[0],
+            launch_init<T>(R.g[lvl(0)], R.gv, R.owned, wrap_depth(R, G_), R.tx, R.ty, R.tz, ct_[0],
                            R.err, s_comp_);
             pack_faces(R, 0, s_comp_, true);
         }
@@ -1548,15 +1600,17 @@ private:
         for (int n = start; n <= K;) {
             // temporal blocking: 3 (tb3) or 2 layers per sweep; shorter tails use the
             // two-layer sweep / a single step (the storage has ghosts for the deepest)
-            const int span = (tbd_ == 3 && n + 2 <= K) ? 3 : ((tb_ && n + 1 <= K) ? 2 : 1);
+            const int span = span_at(n);
             bool comm_follows = false;  // the comm stream already runs behind this layer's shells
             for (int q = n; q < n + span; ++q) guard_checkpoint_level(lvl(q), s_comp_);
             if (cfg_.print_layers && !cfg_.quiet && !capturing_ && ranks_[0].topo.rank == 0)
                 for (int q = n; q < n + span; ++q) std::cout << "calculating layer " << q << "\n";
             mark(s_comp_, 0);
+            // Dirichlet faces of each level buffer on its first write of the solve (the kernels
+            // never store to them; a tb3 C layer is not stored)
             for (int q = n; q < n + span; ++q)
                 for (auto& R : ranks_)
-                    if (q <= L_ || q == start)
+                    if ((first_write_[q + 1] || q == start) && !(span == 3 && q == n))
                         launch_zero_faces<T>(R.g[lvl(q)], R.gv, R.zero_mask, s_comp_);
             if (span == 3 && overlap_) {
                 for (auto& R : ranks_) {
@@ -1815,7 +1869,7 @@ private:
         std::vector<CheckpointHeader> hs;
         std::vector<HostLevel> lps, lcs;
         for (auto& R : ranks_) {
-            const int lp = lvl(n + L_ - 1), lc = lvl(n);
+            const int lp = lvl(n - 1), lc = lvl(n);
             if (!R.pinned) {
                 void* h = nullptr;
                 HIP_CHECK(hipHostMalloc(&h, 2 * R.elems * sizeof(T), hipHostMallocDefault));
@@ -1829,7 +1883,7 @@ private:
             lcs.push_back(host_level(R, R.pinned + R.elems, lc));
         }
         HIP_CHECK(hipEventRecord(ev_ckpt_, s_ckpt_));
-        ckpt_levels_[0] = lvl(n + L_ - 1), ckpt_levels_[1] = lvl(n);
+        ckpt_levels_[0] = lvl(n - 1), ckpt_levels_[1] = lvl(n);
         ckpt_pending_ = true;
         int dev = 0;
         HIP_CHECK(hipGetDevice(&dev));
@@ -1881,8 +1935,9 @@ private:
         std::vector<CheckpointHeader> ex;
         for (auto& R : ranks_) ex.push_back(make_header(cfg_, R.topo, 0, sizeof(T)));
         const int n = agree_resume_layer(cfg_.resume_dir, ex, ext_);  // same layer on every rank
+        plan_slots(n + 1);  // the resumed run's own schedule from layer n + 1
         for (auto& R : ranks_) {
-            const int lp = lvl(n + L_ - 1), lc = lvl(n);
+            const int lp = lvl(n - 1), lc = lvl(n);
             std::vector<T> prev(R.elems, T(0)), cur(R.elems, T(0));
             CheckpointHeader h = make_header(cfg_, R.topo, n, sizeof(T));
             read_checkpoint(cfg_.resume_dir, h, host_level(R, prev, lp), host_level(R, cur, lc),
@@ -1928,11 +1983,20 @@ private:
     bool graph_failed_ = false;
     int G_ = 1;         // ghost depth
     int L_ = 3;         // time levels kept
+    std::vector<int> slot_;          // level buffer of layer n at [n + 1] (plan_slots)
+    std::vector<char> first_write_;  // layer n is the first write of its buffer in the solve
     bool overlap_ = false;
     bool overlap_auto_ = false;   // --overlap auto with a remote halo
-    int trials_done_ = 0;         // overlap auto trials run (on, off)
+    static constexpr int kOverlapTrials = 4;  // overlap auto trial solves: on, off, on, off
+    int trials_done_ = 0;         // overlap auto trials run
     int solves_ = 0;              // solves of this session
-    double trial_ms_[2] = {0, 0};
+    double trial_ms_[kOverlapTrials] = {0, 0, 0, 0};
+    // best (smallest) trial time of an arm (0 on, 1 off) so far, 0 before its first trial
+    double best_trial(int arm) const {
+        double b = 0;
+        for (int q = arm; q < trials_done_; q += 2) b = b > 0 ? std::min(b, trial_ms_[q]) : trial_ms_[q];
+        return b;
+    }
     bool xself_ = false;  // --x-self-transport
     bool direct_ = true;  // --halo direct: single-round deep-halo plan (build_tb_direct)
     static constexpr size_t kMirrorSlots = 2048;

@@ -32,7 +32,8 @@
 #include "device_common.hpp"
 
 // timing ablations of the sweep (tools/ab_tb3_abl.sh builds; never the shipped library):
-// 1 = no error accumulation, 3 = no ring C/D
+// 1 = no error accumulation, 3 = no ring C/D, 4 = every load and store on one fixed plane (no
+// HBM traffic: the compute / LDS / barrier bound), 5 = stores only on one plane, 6 = loads only
 #ifndef W3D_TB3_ABL
 #define W3D_TB3_ABL 0
 #endif
@@ -151,6 +152,15 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WP
     auto prs = [&](const char* base, int i, unsigned nb) {
         return plane_rsrc(base + u64(unsigned(i + p.pbias)) * pbytes, nb);
     };
+    // timing ablations 4-6: loads (A, B) / stores (D, E) pinned to one plane (wrong results)
+    auto prl = [&](const char* base, int i, unsigned nb) {
+        if (W3D_TB3_ABL == 4 || W3D_TB3_ABL == 6) i = ib;
+        return prs(base, i, nb);
+    };
+    auto pst = [&](char* base, int i, unsigned nb) {
+        if (W3D_TB3_ABL == 4 || W3D_TB3_ABL == 5) i = ib;
+        return prs(base, i, nb);
+    };
     auto lrs = [&](const T* plane) { return plane_rsrc(plane - p.poff, pbytes); };
 
     // ---- own nodes ------------------------------------------------------------------------
@@ -239,8 +249,8 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WP
     constexpr int ND = DELTA ? 2 : 1;
     T dm[ND][R], dm1[ND][R], rdm[RP][ND];
     {
-        const auto r0 = prs(p.A, ib - 3, pbytes), rA1 = prs(p.A, ib - 2, pbytes), rA2 = prs(p.A, ib - 1, pbytes);
-        const auto rB = prs(p.B, ib - 2, pbytes);
+        const auto r0 = prl(p.A, ib - 3, pbytes), rA1 = prl(p.A, ib - 2, pbytes), rA2 = prl(p.A, ib - 1, pbytes);
+        const auto rB = prl(p.B, ib - 2, pbytes);
 #pragma unroll
         for (int r = 0; r < R; ++r) {
             a[0][r] = bld<T>(r0, oa[r]);
@@ -395,8 +405,8 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WP
             const bool more = FAST || i <= ie + 1;
             const unsigned nb = more ? pbytes : 0u;
             const int d2 = more ? 2 : 0, d1 = more ? 1 : 0;
-            const auto rA2 = prs(p.A, i + d2, nb);
-            const auto rB1 = prs(p.B, i + d1, nb);
+            const auto rA2 = prl(p.A, i + d2, nb);
+            const auto rB1 = prl(p.B, i + d1, nb);
 #pragma unroll
             for (int r = 0; r < R; ++r) {
                 a[S3][r] = bld<T>(rA2, oa[r]);
@@ -532,14 +542,14 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WP
             }
             if (FAST || (id >= ib && id <= ie)) {
                 if constexpr (!DELTA) {
-                    const auto rd = prs(p.D, id, pbytes);
+                    const auto rd = pst(p.D, id, pbytes);
 #pragma unroll
                     for (int r = 0; r < R; ++r) bst<2>(d[S0][r], rd, os[r]);
                     if (!FAST && (rare & 1)) {
 #pragma unroll
                         for (int g = 0; g < 2; ++g)
                             if (id >= p.wd_lo[g] && id <= p.wd_hi[g]) {
-                                const auto rw = prs(p.D, id + p.wd_sh[g], pbytes);
+                                const auto rw = pst(p.D, id + p.wd_sh[g], pbytes);
 #pragma unroll
                                 for (int r = 0; r < R; ++r) bst<2>(d[S0][r], rw, os[r]);
                             }
@@ -566,27 +576,27 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WP
             }
             if constexpr (DELTA) {
                 // d^{m+2} into the D level (+ its periodic self-wrap), the next sweep's B
-                const auto rd = prs(p.D, ie2, pbytes);
+                const auto rd = pst(p.D, ie2, pbytes);
 #pragma unroll
                 for (int r = 0; r < R; ++r) bst<2>(dm1[H1][r], rd, os[r]);
                 if (!FAST && (rare & 2)) {
 #pragma unroll
                     for (int g = 0; g < 2; ++g)
                         if (ie2 >= p.we_lo[g] && ie2 <= p.we_hi[g]) {
-                            const auto rw = prs(p.D, ie2 + p.we_sh[g], pbytes);
+                            const auto rw = pst(p.D, ie2 + p.we_sh[g], pbytes);
 #pragma unroll
                             for (int r = 0; r < R; ++r) bst<2>(dm1[H1][r], rw, os[r]);
                         }
                 }
             }
-            const auto re = prs(p.E, ie2, pbytes);
+            const auto re = pst(p.E, ie2, pbytes);
 #pragma unroll
             for (int r = 0; r < R; ++r) bst<2>(ev[r], re, os[r]);
             if (!FAST && (rare & 2)) {
 #pragma unroll
                 for (int g = 0; g < 2; ++g)
                     if (ie2 >= p.we_lo[g] && ie2 <= p.we_hi[g]) {
-                        const auto rw = prs(p.E, ie2 + p.we_sh[g], pbytes);
+                        const auto rw = pst(p.E, ie2 + p.we_sh[g], pbytes);
 #pragma unroll
                         for (int r = 0; r < R; ++r) bst<2>(ev[r], rw, os[r]);
                     }

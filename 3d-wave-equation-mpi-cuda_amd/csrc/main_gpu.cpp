@@ -61,7 +61,7 @@ int main(int argc, char** argv) {
                 std::cout << "Process " << rank << " local rank = " << local << " local size = "
                           << env_int("LOCAL_WORLD_SIZE", world) << " hostname = " << host_name()
                           << " device = " << c.device << std::endl;
-            RcclTransport tr(rank, world, id, c.device);
+            RcclTransport tr(rank, world, id, c.device, rccl_max_ctas(overlap_mode(c)));
             RunResult r = run_hip(c, &tr);
             finish(c, r, rank == 0);
             return r.aborted ? 3 : 0;
@@ -87,7 +87,7 @@ int main(int argc, char** argv) {
                     std::cout << "Process " << r << " local rank = " << r << " local size = " << c.Np
                               << " hostname = " << host_name() << " device = " << r << std::endl;
                 }
-                RcclTransport tr(r, c.Np, id, r);
+                RcclTransport tr(r, c.Np, id, r, rccl_max_ctas(overlap_mode(c)));
                 res[r] = run_hip(cr, &tr);
             });
             for (int r = 0; r < c.Np; ++r)  // the first failure is the cause, the rest followed it

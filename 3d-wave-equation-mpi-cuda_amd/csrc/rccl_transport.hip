@@ -58,7 +58,11 @@ int env_int(const char* k, int dflt) {
 }
 }  // namespace
 
-int rccl_max_ctas() { return env_int("WAVE3D_RCCL_MAX_CTAS", kRcclDefaultMaxCtas); }
+int rccl_max_ctas(const std::string& overlap_mode) {
+    const char* e = std::getenv("WAVE3D_RCCL_MAX_CTAS");
+    if (e && *e) return std::max(0, std::atoi(e));
+    return overlap_mode == "off" ? 0 : kRcclOverlapMaxCtas;
+}
 
 // The communicator is non-blocking (config.blocking = 0): initialisation and every enqueue
 // may return ncclInProgress, and settle() polls ncclCommGetAsyncError under the watchdog, so a
@@ -66,7 +70,7 @@ int rccl_max_ctas() { return env_int("WAVE3D_RCCL_MAX_CTAS", kRcclDefaultMaxCtas
 // abort flag), ends the wait with an error instead of a hang. The CTA budget (maxCTAs,
 // WAVE3D_RCCL_MAX_CTAS) caps how many CUs the halo kernels take from the interior sweep
 // that runs concurrently: a face of a few MB needs a few channels, not RCCL's default.
-RcclTransport::RcclTransport(int rank, int size, const std::string& uid, int device)
+RcclTransport::RcclTransport(int rank, int size, const std::string& uid, int device, int max_ctas)
     : impl_(new Impl), rank_(rank), size_(size) {
     W3D_REQUIRE(uid.size() == sizeof(ncclUniqueId), "bad RCCL unique id");
     HIP_CHECK_T(hipSetDevice(device));
@@ -74,7 +78,7 @@ RcclTransport::RcclTransport(int rank, int size, const std::string& uid, int dev
     std::memcpy(&id, uid.data(), sizeof(id));
     ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
     cfg.blocking = 0;
-    const int mx = rccl_max_ctas();
+    const int mx = max_ctas >= 0 ? max_ctas : rccl_max_ctas("auto");
     if (mx > 0) {
         cfg.maxCTAs = mx;
         cfg.minCTAs = std::min(mx, env_int("WAVE3D_RCCL_MIN_CTAS", 1));

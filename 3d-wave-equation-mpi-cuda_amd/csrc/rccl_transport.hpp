@@ -17,17 +17,24 @@ constexpr int kRcclIdBytes = 128;  // sizeof(ncclUniqueId)
 
 std::string rccl_unique_id();  // 128 raw bytes
 
-// CTA budget of the halo communicator: WAVE3D_RCCL_MAX_CTAS, default kRcclDefaultMaxCtas
-// (<= 0: RCCL's own default)
-constexpr int kRcclDefaultMaxCtas = 8;
-int rccl_max_ctas();
+// CTA budget (ncclConfig_t::maxCTAs) of the halo communicator, fixed when it is created:
+// WAVE3D_RCCL_MAX_CTAS when set (<= 0: RCCL's own budget), else by the run's overlap mode —
+//   off       -> 0: RCCL's own budget. Nothing runs beside the exchange, so a cap could only
+//                slow it (a 2x2x2 rank posts 7 peers' messages in one group).
+//   on, auto  -> kRcclOverlapMaxCtas: the interior sweep runs concurrently on the compute
+//                stream, and each halo CTA holds a CU the sweep's workgroups then wait for.
+// One MI355X cannot tell the budgets apart (profiles/rccl_ctas_r3.txt: a 1-rank self-send
+// costs the same at 1..8 CTAs and at the default); the JSON records the budget of every run.
+constexpr int kRcclOverlapMaxCtas = 8;
+int rccl_max_ctas(const std::string& overlap_mode = "auto");
 // Watchdog limit of host-level collectives (WAVE3D_HOST_WATCHDOG_S, default 1800 s)
 double host_collective_limit_s();
 
 class RcclTransport : public Transport {
 public:
     // Must be called with `device` as the current device on this thread.
-    RcclTransport(int rank, int size, const std::string& unique_id, int device);
+    // max_ctas < 0: rccl_max_ctas("auto")
+    RcclTransport(int rank, int size, const std::string& unique_id, int device, int max_ctas = -1);
     ~RcclTransport() override;
     std::string name() const override { return "rccl"; }
     int rank() const override { return rank_; }
@@ -47,6 +54,7 @@ public:
     // peer ends the run with an error instead of a hang.
     bool wait_stream(void* stream, const std::function<long()>* progress = nullptr) override;
     int max_ctas() const;  // CTA budget the communicator was created with (0 = RCCL default)
+    int cta_budget() const override { return max_ctas(); }
     static double init_limit_s();  // WAVE3D_RCCL_INIT_S, default 120 s
 
 private:

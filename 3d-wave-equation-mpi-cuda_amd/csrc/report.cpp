@@ -99,7 +99,10 @@ std::string json_summary(const Config& c, const RunResult& r) {
       << "\", \"transport\": \"" << r.transport << "\""
       << ", \"overlap\": " << (r.overlap ? "true" : "false") << ", \"overlap_mode\": \"" << r.overlap_mode
       << "\", \"overlap_trial_ms\": [" << jnum(r.overlap_trial_ms[0]) << ", " << jnum(r.overlap_trial_ms[1]) << "]"
-      << ", \"comm_size\": " << r.comm_size << ", \"halo_checked\": " << r.halo_checked
+      << ", \"overlap_trials_ms\": [" << jnum(r.overlap_trials[0]) << ", " << jnum(r.overlap_trials[1]) << ", "
+      << jnum(r.overlap_trials[2]) << ", " << jnum(r.overlap_trials[3]) << "]"
+      << ", \"comm_size\": " << r.comm_size << ", \"rccl_max_ctas\": " << r.rccl_max_ctas
+      << ", \"halo_checked\": " << r.halo_checked
       << ", \"rccl_mirror_msgs\": " << r.rccl_mirror_msgs
       << ", \"courant\": " << jnum(r.courant) << ", \"total_ms\": " << jnum(r.t.total_ms)
       << ", \"init_ms\": " << jnum(r.t.init_ms) << ", \"loop_ms\": " << jnum(r.t.loop_ms)

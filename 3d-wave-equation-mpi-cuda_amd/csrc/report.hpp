@@ -40,8 +40,10 @@ struct RunResult {
     bool graph = false;  // time loop replayed as one hipGraph
     bool overlap = false;  // interior/shell split with the halo on a second stream (effective)
     std::string overlap_mode = "off";  // "on" | "off" | "auto" (requested; "none" = no halo)
-    double overlap_trial_ms[2] = {0, 0};  // --overlap auto: solve time with overlap on / off
+    double overlap_trial_ms[2] = {0, 0};  // --overlap auto: best trial solve time, overlap on / off
+    double overlap_trials[4] = {0, 0, 0, 0};  // every trial in order: on, off, on, off
     int comm_size = 0;     // ranks the transport's communicator reports (ncclCommCount), 0 = none
+    int rccl_max_ctas = -1;  // CTA budget of the RCCL communicator (0 = RCCL's own), -1 = none
     long rccl_mirror_msgs = 0;  // --rccl-mirror: messages sent through RCCL and compared
     long long overlap_interior = -1;  // min over ranks of nodes in the interior box that runs
                                       // concurrently with the halo (tb2/tb3: per sweep; -1: none)

@@ -54,7 +54,9 @@ Layout plan_layout(const Config& c, int world) {
     if (auto_tb && !(c.delta && c.dtype == DType::F64)) l.waves = 8;
     if (l.tb && !auto_tb) parse_tb(c.kernel, l.rows, l.waves, l.occ, l.kwaves);
     l.G = l.depth;      // ghost depth = layers per sweep
-    l.L = l.depth + 2;  // 3 / 4 / 5 time levels (tb3: C never stored, D and E written)
+    // time levels: one stored layer per single step -> 3; a sweep stores two layers (tb2: u^m and
+    // u^{m+1}; tb3: D and E, C never stored) and reads two -> 4 (hip_solver plan_slots)
+    l.L = l.depth == 1 ? 3 : 4;
     for (int a = 0; a < 3; ++a) l.dims[a] = c.dims[a];
     (void)world;
     return l;

@@ -60,15 +60,17 @@ def broadcast_bytes(b: bytes | None, src: int = 0, group=None) -> bytes:
     return obj[0]
 
 
-def rccl_transport(device: int | None = None, group=None):
-    """Native RCCL transport for this rank; the unique id travels via torch.distributed."""
+def rccl_transport(device: int | None = None, group=None, overlap: str = "auto"):
+    """Native RCCL transport for this rank; the unique id travels via torch.distributed. The
+    communicator's CTA budget follows the run's overlap mode (C.rccl_max_ctas: RCCL's own budget
+    when overlap is off, a cap when the interior sweep runs beside the halo)."""
     C = load()
     rank, world = dist.get_rank(group), dist.get_world_size(group)
     if device is None:
         device = torch.cuda.current_device()
     uid = C.rccl_unique_id() if rank == 0 else None
     uid = broadcast_bytes(uid, 0, group)
-    return C.RcclTransport(rank, world, uid, device)
+    return C.RcclTransport(rank, world, uid, device, C.rccl_max_ctas(overlap))
 
 
 def _host_view(addr: int, nbytes: int) -> torch.Tensor:
@@ -192,10 +194,10 @@ class TorchStagedTransport:
         return _S(group)
 
 
-def make_transport(kind: str, backend: str = "hip"):
+def make_transport(kind: str, backend: str = "hip", overlap: str = "auto"):
     """'rccl' (native, one GPU per rank), 'staged' (device via gloo), 'gloo' (host, CPU)."""
     if kind == "rccl":
-        return rccl_transport(torch.cuda.current_device())
+        return rccl_transport(torch.cuda.current_device(), overlap=overlap)
     if kind == "staged":
         return TorchStagedTransport()
     if kind in ("gloo", "host"):

@@ -16,8 +16,9 @@ the reference (the reference's errors are identical for every P
     8 GPUs: N=1024, 2x2x2 blocks   (config 4)      golden 8.04265e-08   weak vs 1 GPU
 
 The decomposition is MPI_Dims_create's, as in the reference (mpi_new.cpp:409-433); `--dims`
-overrides it. The default kernel is temporal blocking (2 layers per sweep, 16 instead of
-24 B/node/layer) with 2-deep RCCL halos; `--kernel march2` selects the single-step kernel.
+overrides it. The default kernel is three-layer temporal blocking (tb3: 3 layers per sweep,
+~10.7 instead of 24 B/node/layer, 4 time levels) with 3-deep RCCL halos; `--kernel tb2` selects
+two-layer blocking, `--kernel march2` the single-step kernel.
 The JSON line states what ran: N and dtype in the metric, dims, the effective overlap,
 the transport and the ranks RCCL itself reports (ncclCommCount), and whether the L-inf
 matches the golden. Data: the analytic initial condition on a synthetic grid (the
@@ -44,7 +45,7 @@ def main() -> int:
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5, help="timed solves")
     ap.add_argument("--warmup", type=int, default=3,
-                    help="untimed solves (with halos, solves 2 and 3 are the --overlap auto trials)")
+                    help="untimed solves (with halos, solves 2-5 are the --overlap auto trials)")
     ap.add_argument("--N", type=int, default=0, help="override global N (default: the BASELINE config)")
     ap.add_argument("--config", default="",
                     help="run a named BASELINE config instead (models/presets.py CONFIGS, e.g. "
@@ -58,7 +59,7 @@ def main() -> int:
     ap.add_argument("--scheme", default="auto", choices=["auto", "leapfrog", "delta"],
                     help="time stepping: leapfrog (the reference's), delta (increment form, same scheme "
                          "without the 2u-u cancellation); auto = leapfrog for fp64, delta for fp32 "
-                         "(profiles/fp32_scheme_r3.txt)")
+                         "(profiles/fp32_accuracy_r2.txt, fp32_scheme_r4.txt)")
     ap.add_argument("--math", default="auto", choices=["auto", "exact", "fma"],
                     help="stencil arithmetic: exact = the reference CPU programs' operation order, bit for "
                          "bit; fma = coef/h^2 folded into fused multiply-adds (same scheme, same L-inf abs to "
@@ -120,7 +121,7 @@ def main() -> int:
             print(f"bench: rank {rank}: WAVE3D_BENCH_FAIL_RANK", file=sys.stderr)
             return 3
         if a.backend == "hip":
-            transport = wdist.make_transport(a.transport)
+            transport = wdist.make_transport(a.transport, overlap="off" if a.no_overlap else a.overlap)
         else:
             transport = wdist.TorchHostTransport()
     elif a.backend == "hip":
@@ -177,10 +178,10 @@ def main() -> int:
             dist.barrier()
 
     res = None
-    # --overlap auto with remote halos times its two arms on solves 2 and 3 (solve 1 warms up):
-    # with fewer than 3 warm-up solves the missing trial solves run here, untimed, so the timed
-    # solves all use the chosen arm (reported as "tuning_solves")
-    tuning = (max(0, 3 - a.warmup) if a.backend == "hip" and world > 1 and not a.no_overlap
+    # --overlap auto with remote halos times its two arms twice each on solves 2-5 (solve 1 warms
+    # up): with fewer than 5 warm-up solves the missing trial solves run here, untimed, so the
+    # timed solves all use the chosen arm (reported as "tuning_solves")
+    tuning = (max(0, 5 - a.warmup) if a.backend == "hip" and world > 1 and not a.no_overlap
               and a.overlap == "auto" else 0)
     for _ in range(tuning + a.warmup):
         res = sess.solve(args)
@@ -230,7 +231,8 @@ def main() -> int:
             "kernel": res["kernel"],
             "overlap": bool(res["overlap"]),  # effective (off when there is no remote halo)
             "overlap_mode": res.get("overlap_mode"),
-            "overlap_trial_ms": list(res.get("overlap_trial_ms", (0, 0))),
+            "overlap_trial_ms": list(res.get("overlap_trial_ms", (0, 0))),  # best of two per arm
+            "overlap_trials_ms": list(res.get("overlap_trials_ms", (0, 0, 0, 0))),
             "transport": res["transport"],
             "hip_graph": bool(res.get("graph", False)),
             "fill_hbm": a.fill_hbm or None,
@@ -239,6 +241,8 @@ def main() -> int:
         },
         # ranks the halo communicator spans as RCCL reports them (ncclCommCount), None without one
         "rccl_nranks": res["comm_size"] if res["transport"] == "rccl" else None,
+        # CTA budget the halo communicator was created with (0 = RCCL's own; rccl_transport.hpp)
+        "rccl_max_ctas": res.get("rccl_max_ctas") if res["transport"] == "rccl" else None,
         # halo messages checked at setup with position-encoded patterns (hip_solver.hip)
         "halo_checked": res.get("halo_checked", 0),
         "launch": "self" if os.environ.get("WAVE3D_SELF_LAUNCH") else ("torchrun" if world > 1 else "single"),
@@ -257,18 +261,35 @@ def main() -> int:
     del sess
     import gc
     gc.collect()
-    if a.dtype == "fp32" and a.fp64_ref != "off" or a.fp64_ref == "on":
+    want_ref = a.fp64_ref == "on" or (a.dtype == "fp32" and a.fp64_ref == "auto" and not a.fill_hbm)
+    if want_ref:
         # the fp64 L-inf of the same N, K and decomposition (config 5 compares
-        # against its own fp64 run), after the timed region and after the fp32 session is freed
+        # against its own fp64 run), after the timed region and after the fp32 session is freed.
+        # auto skips it with --fill-hbm (N is sized to the fp32 footprint, fp64 needs twice that)
+        # and when the fp64 levels do not fit the free HBM; a failed reference solve leaves
+        # linf_fp64_ref null — the timed result is printed either way.
+        out["linf_fp64_ref"] = None
         p64 = wave3d.WaveProblem(N, timesteps=a.timesteps, dtype="fp64", math=presets.default_math(a.backend, "fp64"))
-        s64 = wave3d.WaveSolver(p64, a.backend, transport=transport, Np=n_gpus, kernel="auto", dims=dims,
-                                overlap="off" if a.no_overlap else a.overlap,
-                                device=(torch.cuda.current_device() if a.backend == "hip" else None))
-        r64 = s64.run()
-        out["linf_fp64_ref"] = r64.linf_abs
-        out["linf_fp64_ref_kernel"] = r64.kernel
-        out["linf_vs_fp64"] = round(out["linf_abs"] / r64.linf_abs, 3) if r64.linf_abs > 0 else None
-        del s64
+        try:
+            s64 = wave3d.WaveSolver(p64, a.backend, transport=transport, Np=n_gpus, kernel="auto", dims=dims,
+                                    overlap="off" if a.no_overlap else a.overlap,
+                                    device=(torch.cuda.current_device() if a.backend == "hip" else None))
+            need = C.memory_plan(s64.args(), n_gpus)["bytes_per_rank"] if a.backend == "hip" else 0
+            free = torch.cuda.mem_get_info()[0] if a.backend == "hip" else 1 << 62
+            fits = torch.tensor([1.0 if need < 0.95 * free else 0.0])
+            if world > 1:  # every rank runs the reference solve, or none does
+                fits = fits.cuda() if a.backend == "hip" and a.transport == "rccl" else fits
+                dist.all_reduce(fits, op=dist.ReduceOp.MIN)
+            if float(fits.item()) < 1.0:
+                out["linf_fp64_ref_skipped"] = f"fp64 levels need {need / 1e9:.1f} GB, {free / 1e9:.1f} GB free"
+            else:
+                r64 = s64.run()
+                out["linf_fp64_ref"] = r64.linf_abs
+                out["linf_fp64_ref_kernel"] = r64.kernel
+                out["linf_vs_fp64"] = round(out["linf_abs"] / r64.linf_abs, 3) if r64.linf_abs > 0 else None
+            del s64
+        except Exception as e:  # noqa: BLE001 — the reference is an extra, never the result
+            out["linf_fp64_ref_skipped"] = f"reference solve failed: {e}"[:300]
         gc.collect()
     if rank == 0:
         print(json.dumps(out), flush=True)
@@ -295,28 +316,30 @@ def launch_ranks(n: int, argv: list[str], timeout: float) -> int:
     LOCAL_RANK, LOCAL_WORLD_SIZE, MASTER_ADDR=127.0.0.1, MASTER_PORT) and relay rank 0's stdout.
     The parent never imports torch or touches a GPU. The first rank to fail (or the timeout)
     ends the job: the other ranks are terminated at once instead of waiting in a collective,
-    and the exit status is the failed rank's."""
+    and the exit status is the failed rank's. The ranks run in their own sessions (a rank's
+    process group is killed as a whole), so they never outlive this launcher: SIGINT / SIGTERM
+    and any exit path stop them, and each rank gets SIGKILL from the kernel if the launcher
+    itself dies (PR_SET_PDEATHSIG)."""
     import signal
     import subprocess
     import threading
 
+    def die_with_parent():  # runs in the child between fork and exec
+        try:
+            import ctypes
+
+            libc = ctypes.CDLL(None, use_errno=True)
+            libc.prctl(1, signal.SIGKILL, 0, 0, 0)  # PR_SET_PDEATHSIG
+        except Exception:  # noqa: BLE001 — best effort (non-Linux)
+            pass
+
     port = _free_port()
     procs = []
-    for r in range(n):
-        env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(n), LOCAL_RANK=str(r),
-                   LOCAL_WORLD_SIZE=str(n), GROUP_RANK="0", MASTER_ADDR="127.0.0.1",
-                   MASTER_PORT=str(port), WAVE3D_SELF_LAUNCH="1")
-        procs.append(subprocess.Popen([sys.executable, "-u", os.path.abspath(__file__)] + argv, env=env,
-                                      stdout=subprocess.PIPE if r == 0 else subprocess.DEVNULL,
-                                      start_new_session=True, text=True))
 
     def relay():
         for line in procs[0].stdout:
             sys.stdout.write(line)
             sys.stdout.flush()
-
-    th = threading.Thread(target=relay, daemon=True)
-    th.start()
 
     def stop_all():
         for p in procs:
@@ -336,25 +359,46 @@ def launch_ranks(n: int, argv: list[str], timeout: float) -> int:
                     pass
                 p.wait()
 
+    def on_signal(signum, _frame):
+        raise KeyboardInterrupt(f"signal {signum}")
+
+    old = {s: signal.signal(s, on_signal) for s in (signal.SIGINT, signal.SIGTERM)}
     t0 = time.time()
     rc = 0
-    while True:
-        codes = [p.poll() for p in procs]
-        failed = [(r, c) for r, c in enumerate(codes) if c not in (None, 0)]
-        if failed:
-            r, rc = failed[0]
-            print(f"bench: rank {r} exited with status {rc}; stopping the other ranks", file=sys.stderr)
-            stop_all()
-            break
-        if all(c == 0 for c in codes):
-            break
-        if time.time() - t0 > timeout:
-            print(f"bench: ranks still running after {timeout:.0f} s; stopping them", file=sys.stderr)
-            stop_all()
-            rc = 124
-            break
-        time.sleep(0.05)
-    th.join(timeout=5)
+    th = None
+    try:
+        for r in range(n):
+            env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(n), LOCAL_RANK=str(r),
+                       LOCAL_WORLD_SIZE=str(n), GROUP_RANK="0", MASTER_ADDR="127.0.0.1",
+                       MASTER_PORT=str(port), WAVE3D_SELF_LAUNCH="1")
+            procs.append(subprocess.Popen([sys.executable, "-u", os.path.abspath(__file__)] + argv, env=env,
+                                          stdout=subprocess.PIPE if r == 0 else subprocess.DEVNULL,
+                                          start_new_session=True, text=True, preexec_fn=die_with_parent))
+        th = threading.Thread(target=relay, daemon=True)
+        th.start()
+        while True:
+            codes = [p.poll() for p in procs]
+            failed = [(r, c) for r, c in enumerate(codes) if c not in (None, 0)]
+            if failed:
+                r, rc = failed[0]
+                print(f"bench: rank {r} exited with status {rc}; stopping the other ranks", file=sys.stderr)
+                break
+            if all(c == 0 for c in codes):
+                break
+            if time.time() - t0 > timeout:
+                print(f"bench: ranks still running after {timeout:.0f} s; stopping them", file=sys.stderr)
+                rc = 124
+                break
+            time.sleep(0.05)
+    except KeyboardInterrupt as e:
+        print(f"bench: interrupted ({e}); stopping the ranks", file=sys.stderr)
+        rc = 130
+    finally:
+        stop_all()  # no-op for ranks that already exited
+        for s, h in old.items():
+            signal.signal(s, h)
+    if th is not None:
+        th.join(timeout=5)
     return rc if rc > 0 else (1 if rc < 0 else 0)
 
 

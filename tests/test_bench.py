@@ -68,6 +68,36 @@ def test_bench_cpu_two_ranks_gloo():
     assert r["tuning_solves"] == 0  # no overlap trials on the CPU backend
 
 
+@pytest.mark.parametrize("sig", ["SIGTERM", "SIGKILL"])
+def test_bench_self_launch_ranks_die_with_launcher(sig):
+    """ranks of a self-launched job (own sessions) never outlive the launcher. SIGTERM:
+    the launcher's handler stops every rank's process group; SIGKILL (no handler runs): the
+    kernel kills each rank (PR_SET_PDEATHSIG)."""
+    import signal
+    import time
+
+    import psutil
+
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--backend", "cpu", "--N", "96",
+           "--timesteps", "400", "--steps", "50", "--warmup", "0"]
+    p = subprocess.Popen(cmd, cwd=ROOT, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
+    try:
+        kids, t_end = [], time.time() + 60
+        while time.time() < t_end and len(kids) < 2:
+            kids = psutil.Process(p.pid).children()
+            time.sleep(0.1)
+        assert len(kids) == 2
+        time.sleep(3)  # the ranks are up and solving
+        assert all(k.is_running() for k in kids)
+        os.kill(p.pid, getattr(signal, sig))
+        p.wait(timeout=60)
+        _, alive = psutil.wait_procs(kids, timeout=30)
+        assert not alive, f"ranks outlived the launcher: {[k.pid for k in alive]}"
+    finally:
+        if p.poll() is None:
+            p.kill()
+
+
 @pytest.mark.gpu
 def test_bench_gpu_default_config_short():
     r = _bench(["--steps", "1", "--warmup", "1"])
@@ -108,7 +138,7 @@ def test_bench_gpu_multirank_plan_staged(n, N, dims, golden):
     assert r["config"]["timesteps"] == 100 and r["linf_golden"] == golden and r["linf_ok"] is True
     assert r["halo_checked"] > 0 and r["value"] > 0
     assert r["config"]["overlap_mode"] == "auto" and min(r["config"]["overlap_trial_ms"]) > 0
-    assert r["warmup"] == 2 and r["tuning_solves"] == 1  # the second trial solve ran untimed
+    assert r["warmup"] == 2 and r["tuning_solves"] == 3  # trial solves 3-5 ran untimed
     assert r["timers_ms"]["exchange_ms"] > 0 and r["timers_ms"]["comm_ms"] > 0
 
 
@@ -170,7 +200,7 @@ def test_bench_gpu_self_launch_two_ranks_staged():
     r = _bench(["--steps", "1", "--warmup", "0", "--transport", "staged", "--shared-device"], nproc=2,
                timeout=600, self_launch=True)
     _check(r, 2, 1, 0)
-    assert r["tuning_solves"] == 3  # overlap auto: warm-up + both trials before the timed solve
+    assert r["tuning_solves"] == 5  # overlap auto: warm-up + two trials per arm before the timed solve
     assert r["launch"] == "self" and r["config"]["N"] == 512 and r["config"]["dims"] == [2, 1, 1]
     assert r["config"]["timesteps"] == 100 and r["linf_ok"] is True
     assert r["halo_checked"] > 0

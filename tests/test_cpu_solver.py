@@ -136,6 +136,31 @@ def test_checkpoint_resume_delta_scheme(C, tmp_path):
                resume=str(tmp_path))
 
 
+def test_checkpoint_records_math_mode(C, tmp_path):
+    """The header records --math: an fma run neither resumes from an exact run's
+    checkpoints nor prunes them, and the exact run still resumes bitwise afterwards."""
+    import wave3d
+
+    d = str(tmp_path)
+    exact = wave3d.WaveProblem(20, timesteps=14, ic="shifted")
+    fma = wave3d.WaveProblem(20, timesteps=14, ic="shifted", math="fma")
+    full = _solve(exact, ranks=2)
+    _solve(exact, ranks=2, checkpoint_every=6, checkpoint_dir=d)
+    for r in range(2):
+        assert C.checkpoint_layers(d, r) == [6, 12]
+    with pytest.raises(Exception):
+        _solve(fma, ranks=2, resume=d)
+    # an fma run checkpointing into the same directory leaves the exact files alone
+    _solve(fma, ranks=2, checkpoint_every=5, checkpoint_dir=d)
+    for r in range(2):
+        assert C.checkpoint_layers(d, r) == [5, 6, 10, 12]
+    res = _solve(exact, ranks=2, resume=d)
+    assert res.extra["resumed_from"] == 12
+    assert res.max_abs == full.max_abs and res.max_rel == full.max_rel
+    resf = _solve(fma, ranks=2, resume=d)
+    assert resf.extra["resumed_from"] == 10 and resf.extra["math"] == "fma"
+
+
 def test_checkpoint_generations_and_agreed_resume(C, tmp_path):
     """Two complete generations per rank are kept; a rank whose newest file is missing (a crash
     while writing it) makes every rank resume from the newest layer they all have."""

@@ -101,9 +101,23 @@ def test_rccl_self_send(C, single_cpu, kernel, overlap):
     r = torchrun(1, ["--backend", "hip", "--transport", "rccl"], ARGS + extra)
     assert r["transport"] == "rccl" and r["comm_size"] == 1 and r["kernel"] == kernel
     assert r["overlap"] == overlap
+    assert r["rccl_max_ctas"] == (C.rccl_max_ctas("auto") if overlap else 0)
     assert r["exchange_ms"] > 0  # halo messages were timed on the stream
     assert r["max_abs"] == single_cpu["max_abs"] and r["max_rel"] == single_cpu["max_rel"]
 
+
+
+def test_rccl_cta_budget_follows_overlap(C, monkeypatch):
+    """the halo communicator's CTA budget is RCCL's own (0) when nothing runs beside
+    the exchange (overlap off) and a cap when the interior sweep does (on / auto);
+    WAVE3D_RCCL_MAX_CTAS overrides both. Every run's JSON records the budget it got."""
+    monkeypatch.delenv("WAVE3D_RCCL_MAX_CTAS", raising=False)
+    assert C.rccl_max_ctas("off") == 0
+    assert C.rccl_max_ctas("on") == 8 and C.rccl_max_ctas("auto") == 8
+    monkeypatch.setenv("WAVE3D_RCCL_MAX_CTAS", "3")
+    assert C.rccl_max_ctas("off") == 3 and C.rccl_max_ctas("auto") == 3
+    monkeypatch.setenv("WAVE3D_RCCL_MAX_CTAS", "0")
+    assert C.rccl_max_ctas("on") == 0
 
 
 def test_watchdog_is_progress_based(C):

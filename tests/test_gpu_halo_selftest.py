@@ -100,12 +100,14 @@ def test_rccl_mirror_every_message_shape(gpu_prog, cpu_prog, dims, kernel, dtype
 
 
 def test_overlap_auto_trials_then_keeps_the_faster(gpu_prog):
-    """--overlap auto (the default): solve 1 warms up, solve 2 runs overlapped, solve 3 not,
-    later solves use the arm with the shorter (max-over-ranks) time; the JSON records both trial
-    times."""
-    out, _ = _run(gpu_prog, "2,2,2", "tb2", "fp64", ["--repeat", "4"])
+    """--overlap auto (the default): solve 1 warms up, solves 2-5 run overlapped / not / overlapped
+    / not, later solves use the arm with the shorter best-of-two (max-over-ranks) time; the JSON
+    records every trial and the best per arm."""
+    out, _ = _run(gpu_prog, "2,2,2", "tb2", "fp64", ["--repeat", "6"])
     assert out.returncode == 0, out.stderr[-2000:]
     r = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][0])
     on, off = r["overlap_trial_ms"]
-    assert r["overlap_mode"] == "auto" and on > 0 and off > 0
+    trials = r["overlap_trials_ms"]
+    assert r["overlap_mode"] == "auto" and on > 0 and off > 0 and min(trials) > 0
+    assert on == min(trials[0], trials[2]) and off == min(trials[1], trials[3])
     assert r["overlap"] == (on <= off)
