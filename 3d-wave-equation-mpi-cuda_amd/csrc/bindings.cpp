@@ -284,6 +284,52 @@ void k_tb3_dense(int rows, int waves, bool fm, bool first, uintptr_t A, uintptr_
     if (e != hipSuccess) throw Error(std::string("k_tb3: ") + hipGetErrorString(e));
 }
 
+// One deep sweep (k_tbn, `depth` layers): layers m .. m+depth-3 errors only, O0 = u^{m+depth-2},
+// O1 = u^{m+depth-1}; coefs[l] = (hx2, hy2, hz2, coef, ct) and err[l] of layer m+l.
+template <class T>
+void k_tbn_dense(int depth, int rows, int waves, bool fm, bool first, uintptr_t A, uintptr_t B, uintptr_t O0,
+                 uintptr_t O1, const std::vector<i64>& g, const std::vector<std::vector<int>>& boxes,
+                 const std::vector<int>& cdom, int ei0, int ei1, uintptr_t tx, uintptr_t ty, uintptr_t tz,
+                 const std::vector<std::vector<double>>& coefs, const std::vector<uintptr_t>& err, int chunk,
+                 uintptr_t stream) {
+    i64 o = 0;
+    const GridView v = gview_g(g, o);
+    W3D_REQUIRE(int(coefs.size()) == depth && int(err.size()) == depth, "k_tbn: one coefficient set / slot per layer");
+    std::vector<Box> bx;
+    for (auto& b : boxes) bx.push_back(tobox(b));
+    StepCoefs cs[kTbnMaxDepth];
+    u64* es[kTbnMaxDepth] = {};
+    for (int l = 0; l < depth; ++l) cs[l] = tocoefs(coefs[l]), es[l] = P<u64>(err[l]);
+    const hipStream_t s = (hipStream_t)stream;
+    T* txy = nullptr;
+    T* rt = nullptr;
+    const size_t ntxy = txy_elems(v.X, v.Y), ntz = size_t(v.Z) + 2;
+    if (hipMalloc(&txy, ntxy * sizeof(T)) != hipSuccess) throw Error("k_tbn: hipMalloc failed");
+    if (fm && hipMalloc(&rt, (2 * ntxy + ntz) * sizeof(T)) != hipSuccess) {
+        (void)hipFree(txy);
+        throw Error("k_tbn: hipMalloc failed");
+    }
+    try {
+        launch_txy<T>(txy, P<T>(tx), P<T>(ty), v.X, v.Y, s);
+        if (fm) {
+            launch_txr<T>(rt, txy, ntxy, s);
+            launch_recip_abs<T>(rt + 2 * ntxy, P<T>(tz), ntz, s);
+        }
+        launch_tbn<T>(depth, rows, waves, fm, first, P<T>(A) + o, P<T>(B) + o, P<T>(O0) + o, P<T>(O1) + o, v,
+                      bx.data(), int(bx.size()), tobox(cdom), ei0, ei1, Wrap{}, Wrap{}, TbnSeam<T>{}, txy, P<T>(tz),
+                      rt, fm ? rt + 2 * ntxy : nullptr, cs, es, chunk, s);
+    } catch (...) {
+        (void)hipStreamSynchronize(s);
+        (void)hipFree(txy);
+        (void)hipFree(rt);
+        throw;
+    }
+    const hipError_t e = hipStreamSynchronize(s);
+    (void)hipFree(txy);
+    (void)hipFree(rt);
+    if (e != hipSuccess) throw Error(std::string("k_tbn: ") + hipGetErrorString(e));
+}
+
 template <class T>
 void k_init(uintptr_t u, const std::vector<i64>& g, const std::vector<int>& box,
             const std::vector<int>& wrap, uintptr_t tx, uintptr_t ty, uintptr_t tz, double ct0,
@@ -504,6 +550,9 @@ PYBIND11_MODULE(_wave3d_C, m) {
     m.def("k_tb2_f32", &k_tb2_dense<float>);
     m.def("k_tb3_f64", &k_tb3_dense<double>);
     m.def("k_tb3_f32", &k_tb3_dense<float>);
+    m.def("k_tbn_f64", &k_tbn_dense<double>);
+    m.def("k_tbn_f32", &k_tbn_dense<float>);
+    m.def("tbn_supported", &tbn_supported);
     m.def("tb_supported", [](int depth, int rows, int waves, int nwk, bool fm) {
         return depth == 3 ? tb3_supported(rows, waves, fm) : tb2_supported(rows, waves, 0, nwk);
     }, py::arg("depth"), py::arg("rows"), py::arg("waves"), py::arg("nwk") = 1, py::arg("fm") = false);

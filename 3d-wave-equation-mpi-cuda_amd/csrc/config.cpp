@@ -13,7 +13,7 @@ std::string usage() {
            "  --math exact|fma       exact = the reference's operation order, bit for bit (default);\n"
            "                         fma = coef/h^2 folded into fused multiply-adds (tb3 kernels)\n"
            "  --pi ref|exact         ref = 3.1415926535 as the reference CPU programs (default)\n"
-           "  --scheme leapfrog|delta  delta = increment form (fp32 accuracy; tb2 kernels, CPU)\n"
+           "  --scheme leapfrog|delta  delta = increment form (fp32 accuracy; tb2 / tb3 kernels, CPU)\n"
            "  --ic ref|shifted       shifted = sin(2*pi*x/Lx + 0.7) periodic-BC check\n"
            "  --dims a,b,c           override the Cartesian process grid\n"
            "  --ranks P              simulate P ranks in-process (loopback transport)\n"
@@ -25,7 +25,8 @@ std::string usage() {
            "  --overlap auto|on|off  interior/shell split with the halo on a second stream; auto\n"
            "                         (default) times the first two solves on / off, keeps the faster\n"
            "  --no-overlap           = --overlap off\n"
-           "  --kernel K             auto (tb3; fp64 increment form: tb2r2w4) | tb2[r<R>][w<W>] | tb3[r<R>w<W>] | march[2|4|8][nt|p|f]\n"
+           "  --kernel K             auto (tb3; fp64 increment form: tb2r2w4) | tb2[r<R>][w<W>] | tb3[r<R>w<W>] | tb4\n"
+           "                         | march[2|4|8][nt|p|f]\n"
            "                         | naive | flat   (temporal blocking / single-step variants)\n"
            "  --chunk C              i-planes per marching work item\n"
            "  --format new|omp|cuda|none      output file flavour (default new)\n"
@@ -44,6 +45,9 @@ std::string usage() {
            "  --rccl-mirror          with --ranks P: also send every halo message (and the error\n"
            "                         allreduce) through a 1-rank RCCL communicator, compare bitwise\n"
            "  --no-halo-check        skip the init-time halo self-test (patterns through the real plan)\n"
+           "  --model-link G[,L]     with --ranks P: every loopback exchange also waits the time its\n"
+           "                         busiest peer link needs at G GB/s (+ L us latency), on one CU\n"
+           "                         (an xGMI link model for overlap experiments on one GPU)\n"
            "  --device d  --threads t  --no-print-layers  --quiet\n";
 }
 
@@ -207,6 +211,12 @@ Config parse_cli(const std::vector<std::string>& a) {
             else throw Error("--graph must be on, off or auto");
         } else if (o == "--rccl-mirror") {
             c.rccl_mirror = true;
+        } else if (o == "--model-link") {
+            const std::string v = need(i++);
+            const size_t cm = v.find(',');
+            c.model_link_gbps = std::stod(v.substr(0, cm));
+            c.model_link_lat_us = cm == std::string::npos ? 0.0 : std::stod(v.substr(cm + 1));
+            W3D_REQUIRE(c.model_link_gbps > 0 && c.model_link_lat_us >= 0, "--model-link needs GBPS > 0[,LAT_US >= 0]");
         } else if (o == "--no-halo-check") {
             c.halo_check = false;
         } else if (o == "--fault") {

@@ -66,6 +66,8 @@ struct Config {
     int graph = -1;                 // hipGraph replay of the time loop: 1 on, 0 off, -1 auto
     double fill_hbm = 0;            // >0: replace N by the largest N using this HBM fraction
     bool halo_check = true;         // init-time halo self-test through the real plan/transport
+    double model_link_gbps = 0;     // --model-link: simulated ranks' exchanges also wait the
+    double model_link_lat_us = 0;   // modelled time of their busiest peer link (overlap studies)
     std::string fault;              // fault injection spec, e.g. "drop_face:1:5" (or env WAVE_FI)
     int device = -1;                // explicit device id (default: local rank)
     int threads = 0;                // CPU backend OpenMP threads (0 = Np)

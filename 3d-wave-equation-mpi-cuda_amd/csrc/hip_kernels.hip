@@ -451,6 +451,14 @@ __global__ void k_stamp(u64* ts, int slot) {
     if (threadIdx.x == 0) ts[slot] = wall_clock64();
 }
 
+// Link-time model (--model-link): one wave waits `ticks` of the constant-rate wall clock, then
+// exits — a bounded wait that holds one CU's slot, as the sender/receiver kernels of a remote
+// transfer would, while the data itself moves by the loopback copies after it.
+__global__ void k_spin(u64 ticks) {
+    const u64 t0 = wall_clock64();
+    while (wall_clock64() - t0 < ticks) __builtin_amdgcn_s_sleep(8);
+}
+
 __global__ void k_encode(const double* v, u64* k, int n) {
     const int t = blockIdx.x * blockDim.x + threadIdx.x;
     if (t < n) k[t] = enc_key(v[t]);
@@ -777,6 +785,12 @@ void launch_init_err(u64* err, int layers, hipStream_t s) {
 
 void launch_stamp(u64* ts, int slot, hipStream_t s) {
     hipLaunchKernelGGL(k_stamp, dim3(1), dim3(64), 0, s, ts, slot);
+    HIP_OK(hipGetLastError());
+}
+
+void launch_spin(u64 ticks, hipStream_t s) {
+    if (ticks == 0) return;
+    hipLaunchKernelGGL(k_spin, dim3(1), dim3(64), 0, s, ticks);
     HIP_OK(hipGetLastError());
 }
 

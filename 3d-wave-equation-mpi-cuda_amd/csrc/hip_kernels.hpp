@@ -48,10 +48,10 @@ struct FusedPack {
 
 // Periodic self-wrap fused into the stores (dims[0] == 1): plane `src[q]` is also written
 // to ghost plane `dst[q]` (depth-2 ghosts need 4 pairs). -1 = unused.
-constexpr int kMaxWrap = 6;
+constexpr int kMaxWrap = 8;  // depth-4 ghosts: 4 pairs per side
 struct Wrap {
-    int src[kMaxWrap] = {-1, -1, -1, -1, -1, -1};
-    int dst[kMaxWrap] = {-1, -1, -1, -1, -1, -1};
+    int src[kMaxWrap] = {-1, -1, -1, -1, -1, -1, -1, -1};
+    int dst[kMaxWrap] = {-1, -1, -1, -1, -1, -1, -1, -1};
 };
 
 // Stencil kernel variant: 2.5-D marching (rows per lane, non-temporal u^{n-2} loads) or
@@ -117,7 +117,10 @@ struct SeamCPlane {
     T* out = nullptr;
     const T *Ac = nullptr, *Am = nullptr, *Ap = nullptr, *Bc = nullptr;
 };
-// fm: --math fma instantiations (stencil_math coef_lap_fma), not bitwise with the reference
+// fm: --math fma instantiations (stencil_math coef_lap_fma), not bitwise with the reference.
+// The same operator evaluates any later layer on a partner plane (Ac = layer l-1 there, Am / Ap
+// its x neighbours, Bc = layer l-2): up to kMaxSeamOps planes per launch.
+constexpr int kMaxSeamOps = 6;
 template <class T>
 void launch_seam_c(bool first, bool delta, bool fm, const SeamCPlane<T>* ops, int nops, const GridView& gv,
                    const Box& cdom, const StepCoefs& cC, hipStream_t s);
@@ -129,6 +132,26 @@ void launch_tb3(int rows, int waves, bool delta, bool fm, bool first, const T* A
                 const Wrap& wrapD, const Wrap& wrapE, const SeamPartners<T>& seam, const T* txy,
                 const T* tz, const T* txr, const T* rtz, const StepCoefs& cC, const StepCoefs& cD,
                 const StepCoefs& cE, u64* errC, u64* errD, u64* errE, int chunk, hipStream_t s);
+
+// Deep temporal blocking (hip_tbn.hip): one sweep computes D = depth layers u^m .. u^{m+D-1}
+// from A = u^{m-1}, B = u^{m-2} and stores only the last two (O0 = u^{m+D-2}, O1 = u^{m+D-1}, the
+// next sweep's B and A). Needs ghost depth >= D of A and >= D-1 of B; O0 / O1 get the periodic
+// self-wrap of depth D-1 / D. Periodic seam: at plane next_i the x+ neighbour of layer l is
+// nP[l] (A at the partner plane for l = 0, layer l-1 evaluated there by launch_seam_c for
+// l >= 1); mirrored for prev_i / pP. c[l] / err[l]: coefficients and error slots of layer m+l.
+constexpr int kTbnMaxDepth = 4;
+template <class T>
+struct TbnSeam {
+    int next_i = -(1 << 30), prev_i = -(1 << 30);
+    const T* nP[kTbnMaxDepth - 1] = {};
+    const T* pP[kTbnMaxDepth - 1] = {};
+};
+bool tbn_supported(int depth, int rows, int waves, bool fm);
+template <class T>
+void launch_tbn(int depth, int rows, int waves, bool fm, bool first, const T* A, const T* B, T* O0, T* O1,
+                const GridView& gv, const Box* boxes, int nbox, const Box& cdom, int ei0, int ei1,
+                const Wrap& wrap0, const Wrap& wrap1, const TbnSeam<T>& seam, const T* txy, const T* tz,
+                const T* txr, const T* rtz, const StepCoefs* c, u64* const* err, int chunk, hipStream_t s);
 
 // Box halo staging for the temporal-blocking exchange on y/z splits: copy the logical box
 // `b` of a level (origin `grid` = logical (0,0,0), strides of `gv`) to / from a contiguous
@@ -148,6 +171,8 @@ void launch_box_copy(const BoxCopy<T>* ops, int nops, const GridView& gv, bool t
 void launch_init_err(u64* err, int layers, hipStream_t s);
 // ts[slot] = device wall clock (hipDeviceAttributeWallClockRate kHz) in stream order
 void launch_stamp(u64* ts, int slot, hipStream_t s);
+// one wave spins `ticks` of the device wall clock (hipDeviceAttributeWallClockRate kHz), bounded
+void launch_spin(u64 ticks, hipStream_t s);
 
 // Device encode of a double into the order-preserving key (exposed for tests).
 void launch_encode_keys(const double* v, u64* k, int n, hipStream_t s);

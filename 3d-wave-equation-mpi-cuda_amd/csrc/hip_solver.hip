@@ -45,8 +45,10 @@ using clk = std::chrono::steady_clock;
 
 // Temporal-blocking variant names: "tb2" (2 rows/lane, 4 waves), "tb2r<R>", "tb2r<R>w<W>".
 std::string tb_name(int rows, int waves, int occ, int depth = 2, int kwaves = 1) {
-    if (depth == 3)
-        return rows == 2 && waves == 8 ? "tb3" : "tb3r" + std::to_string(rows) + "w" + std::to_string(waves);
+    if (depth >= 3) {
+        const std::string b = "tb" + std::to_string(depth);
+        return rows == 2 && waves == 8 ? b : b + "r" + std::to_string(rows) + "w" + std::to_string(waves);
+    }
     std::string s = rows == 2 && waves == 4 && occ == 0 && kwaves == 1 ? "tb2" : "tb2r" + std::to_string(rows);
     if (waves != 4 || occ || kwaves != 1) s += "w" + std::to_string(waves);
     if (kwaves != 1) s += "k" + std::to_string(kwaves);
@@ -55,6 +57,7 @@ std::string tb_name(int rows, int waves, int occ, int depth = 2, int kwaves = 1)
 }
 
 constexpr int kMaxLevels = 4;  // time levels: 3 single-step, 4 with two- / three-layer sweeps
+constexpr int kSeamPlanes = 8;  // seam scratch planes: tb3 C at 2 partners; tb4 6 C + 2 D planes
 
 template <class T>
 struct DevRank {
@@ -79,6 +82,7 @@ struct DevRank {
     Wrap wrap;                   // single-step periodic self-wrap (depth 1)
     Wrap wrap2;                  // depth-2 self-wrap (temporal blocking: IC and D layers)
     Wrap wrap3;                  // depth-3 self-wrap (three-layer blocking: IC and E layers)
+    Wrap wrap4;                  // depth-4 self-wrap (four-layer blocking: IC and the last layer)
     Box cdom;                    // temporal blocking: where C is a stencil value
     FusedPack<T> pack;           // pointers into sbuf
     // temporal blocking across ranks (x slabs): plane messages, seam alias plane, boxes
@@ -113,7 +117,8 @@ struct DevRank {
     std::vector<PeerBuf> tb_psends, tb_precvs;
     T* alias_buf = nullptr;      // one plane: x=N (first x-rank) or x=0 (last x-rank)
     T* alias_bufB = nullptr;     // the same plane of the B level (three-layer blocking)
-    T* seamc_buf = nullptr;      // two planes: C on the seam partner planes (three-layer)
+    T* seamc_buf = nullptr;      // earlier layers on the seam partner planes (tb3: 2 planes, tb4: 8)
+    T* seamc_in = nullptr;       // the interior's copy (overlapped self-wrap runs)
     T* pinned = nullptr;         // checkpoint staging (2 levels, pinned host memory)
     Box tb_interior;
     std::vector<Box> tb_shell;
@@ -140,6 +145,7 @@ public:
         const Layout lay = plan_layout(c, world_);
         tb_ = lay.tb;
         tbd_ = lay.depth;
+        tbn_ = lay.generic;
         tb_rows_ = lay.rows;
         tb_waves_ = lay.waves;
         tb_occ_ = lay.occ;
@@ -147,13 +153,17 @@ public:
         G_ = lay.G;
         L_ = lay.L;
         for (int a = 0; a < 3; ++a) cfg_.dims[a] = lay.dims[a];
-        W3D_REQUIRE(!c.fma || !tb_ ||
+        W3D_REQUIRE(tbd_ < 4 || (!c.delta && tbn_supported(4, tb_rows_, tb_waves_, c.fma)),
+                    "four-layer blocking: leapfrog only, tiles " + std::string(tbn_supported(4, 2, 8, c.fma) ? "r2w8" : "none"));
+        W3D_REQUIRE(!c.fma || !tb_ || tbd_ == 4 ||
                         (tbd_ == 3 ? (c.delta ? tb3_delta_supported(tb_rows_, tb_waves_, true)
                                               : tb3_supported(tb_rows_, tb_waves_, true))
                                    : tb_occ_ == 0 && tb2_fma_supported(tb_rows_, tb_waves_, tb_nwk_, c.delta)),
                     "--math fma: no fma instantiation of this temporal-blocking tile (tb3, tb3r1w8, tb3r1w16, "
                     "tb2r2w8, tb2)");
-        W3D_REQUIRE(!tb_ || (tbd_ == 3 ? tb3_supported(tb_rows_, tb_waves_)
+        W3D_REQUIRE(!tbn_ || tbd_ == 4 || (!c.delta && tbn_supported(3, tb_rows_, tb_waves_, c.fma)),
+                    "tbn3: leapfrog, tile r2w8");
+        W3D_REQUIRE(!tb_ || tbd_ == 4 || (tbd_ == 3 ? tb3_supported(tb_rows_, tb_waves_)
                                         : tb2_supported(tb_rows_, tb_waves_, tb_occ_, tb_nwk_)),
                     "wave3d: unknown kernel variant " + c.kernel);
         kind_ = parse_kernel_variant(tb_ ? std::string("auto") : c.kernel);
@@ -247,6 +257,7 @@ public:
         res.dtype = cfg_.dtype;
         res.backend = "hip";
         res.kernel = tb_ ? tb_name(tb_rows_, tb_waves_, tb_occ_, tbd_, tb_nwk_) : kernel_variant_name(kind_);
+        if (tbn_ && tbd_ == 3) res.kernel = "tbn" + res.kernel.substr(2);
         res.courant = prob_.courant;
         res.transport = ext_ ? ext_->name() : (world_ > 1 ? "loopback" : "self");
         // --overlap auto: solves 2..5 are the trials (on, off, on, off; the first solve only warms
@@ -416,7 +427,12 @@ private:
                     R.wrap3.src[q] = X - 3 + q, R.wrap3.dst[q] = -2 + q;
                     R.wrap3.src[3 + q] = 2 + q, R.wrap3.dst[3 + q] = X + 1 + q;
                 }
-                if (tbd_ == 3) W3D_REQUIRE(X >= 7, "three-layer blocking self-wrap needs >= 7 x planes");
+                for (int q = 0; q < 4; ++q) {
+                    R.wrap4.src[q] = X - 4 + q, R.wrap4.dst[q] = -3 + q;
+                    R.wrap4.src[4 + q] = 2 + q, R.wrap4.dst[4 + q] = X + 1 + q;
+                }
+                if (tbd_ >= 3)
+                    W3D_REQUIRE(X >= 2 * tbd_ + 1, "deep temporal blocking self-wrap needs >= 2 x depth + 1 x planes");
                 if (tb_) W3D_REQUIRE(X >= 5, "temporal blocking self-wrap needs >= 5 x planes");
             }
             // stencil-valued region of the blocked layers: C/D/E are evaluated on rings up to
@@ -456,11 +472,16 @@ private:
             if (t.nbr[2][1] >= 0) in.k1 = std::min(in.k1, TKm > 1 ? TKm * ((Z - 1) / TKm) : Z - 1);
             R.interior = in;
             build_tb_plan(R);
-            if (tbd_ == 3 && (R.plan.self_x || t.first(0) || t.last(0))) {
-                // C on the seam partner planes (three-layer sweeps); allocated here, never
-                // inside a hipGraph capture
-                HIP_CHECK(hipMalloc(&R.seamc_buf, 2 * R.gv.si * sizeof(T)));
-                HIP_CHECK(hipMemset(R.seamc_buf, 0, 2 * R.gv.si * sizeof(T)));
+            if (tbd_ >= 3 && (R.plan.self_x || t.first(0) || t.last(0))) {
+                // earlier layers on the seam partner planes (three- / four-layer sweeps);
+                // allocated here, never inside a hipGraph capture
+                const i64 np = kSeamPlanes;
+                HIP_CHECK(hipMalloc(&R.seamc_buf, np * R.gv.si * sizeof(T)));
+                HIP_CHECK(hipMemset(R.seamc_buf, 0, np * R.gv.si * sizeof(T)));
+                if (R.plan.self_x && (t.dims[1] > 1 || t.dims[2] > 1)) {
+                    HIP_CHECK(hipMalloc(&R.seamc_in, np * R.gv.si * sizeof(T)));
+                    HIP_CHECK(hipMemset(R.seamc_in, 0, np * R.gv.si * sizeof(T)));
+                }
             }
             R.shell.clear();
             auto add = [&](Box b) {
@@ -501,6 +522,7 @@ private:
             (void)hipFree(R.alias_buf);
             (void)hipFree(R.alias_bufB);
             (void)hipFree(R.seamc_buf);
+            (void)hipFree(R.seamc_in);
             if (R.pinned) (void)hipHostFree(R.pinned);
             for (int q = 0; q < 2; ++q) {
                 for (auto& m : R.tb_bsends[q]) (void)hipFree(m.buf);
@@ -553,7 +575,10 @@ private:
     }
     // layers computed by the operation that starts at layer n (3: three-layer sweep, 2: two-
     // layer sweep, 1: single step) — the schedule of enqueue_layers()
-    int span_at(int n) const { return (tbd_ == 3 && n + 2 <= prob_.K) ? 3 : ((tb_ && n + 1 <= prob_.K) ? 2 : 1); }
+    int span_at(int n) const {
+        const int left = prob_.K - n + 1;
+        return tb_ ? std::max(1, std::min(tbd_, left)) : 1;
+    }
     // Slot plan of a solve that starts at layer `start` (1, or the layer after a resumed
     // checkpoint): layers start-1 / start-2 in slots 0 / 1; every operation then takes the
     // lowest free slots for the layers it stores. A three-layer sweep's C layer maps to the slot
@@ -570,7 +595,7 @@ private:
         for (int n = start; n <= K;) {
             const int span = span_at(n);
             const int live[2] = {slot_[n], slot_[n - 1]};  // layers n - 1, n - 2
-            const int first_stored = span == 3 ? n + 1 : n;
+            const int first_stored = span >= 2 ? n + span - 2 : n;  // sweeps store their last two
             int l = 0;
             for (int q = first_stored; q < n + span; ++q) {
                 while (l == live[0] || l == live[1]) ++l;
@@ -580,12 +605,12 @@ private:
                 used[l] = 1;
                 ++l;
             }
-            if (span == 3) slot_[n + 1] = slot_[n + 3];
+            for (int q = n; q < first_stored; ++q) slot_[q + 1] = slot_[n + span];  // unstored layers
             n += span;
         }
     }
     const Wrap& wrap_depth(const DevRank<T>& R, int d) const {
-        return d >= 3 ? R.wrap3 : (d == 2 ? R.wrap2 : R.wrap);
+        return d >= 4 ? R.wrap4 : (d == 3 ? R.wrap3 : (d == 2 ? R.wrap2 : R.wrap));
     }
 
     int send_plane(const DevRank<T>& R, int side) const {
@@ -653,7 +678,7 @@ private:
             const bool first = t.first(0) && t.dims[0] > 1, last = t.last(0) && t.dims[0] > 1;
             const bool lastx = t.last(0), firstx = t.first(0);
             const int up = t.nbr[0][1], dn = t.nbr[0][0];
-            const bool aliasB = tbd_ == 3;
+            const bool aliasB = tbd_ >= 3;
             R.tb_sends.push_back(M{up, 11, 0, lastx ? X - dA : X - dA + 1, dA});
             if (last) R.tb_sends.push_back(M{up, 12, 0, X, 1});
             R.tb_sends.push_back(M{up, 13, 1, lastx ? X - dB : X - dB + 1, dB});
@@ -714,7 +739,7 @@ private:
             // three-layer sweeps also evaluate C on the seam alias plane (k_seam_c), whose
             // j/k neighbours at the subdomain edge are ghosts: the alias planes of the y/z
             // neighbours (same x coordinate, so they hold the same global plane) supply them
-            if (tbd_ == 3 && R.alias_buf) {
+            if (tbd_ >= 3 && R.alias_buf) {
                 auto abox = [&](int lo, int hi) {
                     Box b = box(lo, hi);
                     b.i0 = b.i1 = 0;
@@ -821,7 +846,7 @@ private:
             if (alias) lo[0] = hi[0] = d[0] < 0 ? E[0] : 1;  // plane x = N (last) / x = 0 (first)
             return Box{lo[0], hi[0], lo[1], hi[1], lo[2], hi[2]};
         };
-        for (int level = 0; level < (tbd_ == 3 ? 4 : 3); ++level) {
+        for (int level = 0; level < (tbd_ >= 3 ? 4 : 3); ++level) {
             const bool alias = level >= 2;
             if (alias && !seam) continue;
             const int D = (level == 0 || level == 2) ? dA : dB;
@@ -927,6 +952,12 @@ private:
             for (auto& m : R.tb_precvs) rcv.push_back({m.peer, kPeerTag, m.buf, m.count * sizeof(T)});
             if (!snd.empty() || !rcv.empty()) ext_->exchange(snd, rcv, s);
         } else {
+            std::map<std::pair<int, int>, size_t> link;
+            for (auto& S : ranks_) {
+                for (auto& m : S.tb_sends) link[{S.topo.rank, m.peer}] += size_t(m.nplanes) * S.gv.si * sizeof(T);
+                for (auto& m : S.tb_psends) link[{S.topo.rank, m.peer}] += m.count * sizeof(T);
+            }
+            model_link(link, s);
             for (auto& S : ranks_)
                 for (auto& m : S.tb_sends) {
                     auto& D = ranks_[m.peer];
@@ -1124,11 +1155,118 @@ private:
         launch_seam_c<T>(m == 1, cfg_.delta, cfg_.fma, ops.data(), int(ops.size()), R.gv, R.cdom, coefs(m), s);
     }
 
+    // Four-layer sweep m (k_tbn): layers m, m+1 in registers only, m+2 and m+3 stored. The seam
+    // partners are layers m-1 (A), m and m+1 at the partner planes; layer m+1 there needs layer m
+    // at the partner and at both its x neighbours — with the seam rule at the one across the seam
+    // (the ghost copy of global 1 sees x = 0, of N-1 sees x = N): stage 1 evaluates layer m on
+    // those planes (C ops), stage 2 layer m+1 at each partner (D ops), both before the sweep.
+    TbnSeam<T> seam_partners4(DevRank<T>& R, int m, std::vector<SeamCPlane<T>>* c_ops,
+                              std::vector<SeamCPlane<T>>* d_ops) {
+        const T* A = R.g[lvl(m - 1)];
+        const T* B = R.g[lvl(m - 2)];
+        const i64 si = R.gv.si;
+        const int X = R.topo.X();
+        TbnSeam<T> sp;
+        auto scratch = [&](int q) { return R.seamc_buf + i64(q) * si + R.plane_off; };
+        auto op = [&](std::vector<SeamCPlane<T>>* v, int q, const T* c, const T* xm, const T* xp, const T* pw) {
+            W3D_REQUIRE(R.seamc_buf, "seam scratch not allocated");
+            SeamCPlane<T> o;
+            o.out = scratch(q), o.Ac = c, o.Am = xm, o.Ap = xp, o.Bc = pw;
+            if (v) v->push_back(o);
+            return scratch(q);
+        };
+        auto Ap = [&](int i) { return A + i64(i) * si; };
+        auto Bp = [&](int i) { return B + i64(i) * si; };
+        const T* aA = R.alias_buf ? R.alias_buf + R.plane_off : nullptr;
+        const T* aB = R.alias_bufB ? R.alias_bufB + R.plane_off : nullptr;
+        if (R.topo.dims[0] == 1) {
+            // next side (ghost 0 = copy of N-1): partner x = N = plane X
+            const T* cX = op(c_ops, 0, Ap(X), Ap(X - 1), Ap(X + 1), Bp(X));
+            const T* cXm = op(c_ops, 1, Ap(X - 1), Ap(X - 2), Ap(X), Bp(X - 1));
+            const T* cXp = op(c_ops, 2, Ap(X + 1), Ap(1), Ap(X + 2), Bp(X + 1));  // copy of 1: x- = x=0
+            sp.next_i = 0, sp.nP[0] = Ap(X), sp.nP[1] = cX, sp.nP[2] = op(d_ops, 6, cX, cXm, cXp, Ap(X));
+            // prev side (ghost X+1 = copy of 1): partner x = 0 = plane 1
+            const T* c1 = op(c_ops, 3, Ap(1), Ap(0), Ap(2), Bp(1));
+            const T* c0 = op(c_ops, 4, Ap(0), Ap(-1), Ap(X), Bp(0));  // copy of N-1: x+ = x=N
+            const T* c2 = op(c_ops, 5, Ap(2), Ap(1), Ap(3), Bp(2));
+            sp.prev_i = X + 1, sp.pP[0] = Ap(1), sp.pP[1] = c1, sp.pP[2] = op(d_ops, 7, c1, c0, c2, Ap(1));
+        } else if (R.topo.first(0)) {
+            // partner x = N lives on the last x-rank (alias planes); ghost 0 = N-1, plane 2 = global 1
+            const T* cN = op(c_ops, 0, aA, Ap(0), Ap(2), aB);
+            const T* cNm = op(c_ops, 1, Ap(0), Ap(-1), aA, Bp(0));
+            const T* c1 = op(c_ops, 2, Ap(2), Ap(1), Ap(3), Bp(2));
+            sp.next_i = 0, sp.nP[0] = aA, sp.nP[1] = cN, sp.nP[2] = op(d_ops, 6, cN, cNm, c1, aA);
+        } else if (R.topo.last(0)) {
+            // partner x = 0 lives on the first x-rank; plane X-1 = N-1, ghost X+1 = global 1
+            const T* c0 = op(c_ops, 3, aA, Ap(X - 1), Ap(X + 1), aB);
+            const T* cm = op(c_ops, 4, Ap(X - 1), Ap(X - 2), Ap(X), Bp(X - 1));
+            const T* cp = op(c_ops, 5, Ap(X + 1), aA, Ap(X + 2), Bp(X + 1));  // copy of 1: x- = x=0
+            sp.prev_i = X + 1, sp.pP[0] = aA, sp.pP[1] = c0, sp.pP[2] = op(d_ops, 7, c0, cm, cp, aA);
+        }
+        return sp;
+    }
+
+    void seam4(DevRank<T>& R, int m, hipStream_t s) {
+        std::vector<SeamCPlane<T>> c_ops, d_ops;
+        seam_partners4(R, m, &c_ops, &d_ops);
+        launch_seam_c<T>(m == 1, false, cfg_.fma, c_ops.data(), int(c_ops.size()), R.gv, R.cdom, coefs(m), s);
+        launch_seam_c<T>(false, false, cfg_.fma, d_ops.data(), int(d_ops.size()), R.gv, R.cdom, coefs(m + 1), s);
+    }
+
+    void sweep4(DevRank<T>& R, int m, hipStream_t s, const Box* boxes = nullptr, int nbox = 0) {
+        const T* A = R.g[lvl(m - 1)];
+        const T* B = R.g[lvl(m - 2)];
+        const TbnSeam<T> sp = seam_partners4(R, m, nullptr, nullptr);
+        if (!boxes) boxes = &R.compute, nbox = 1;
+        StepCoefs c[4];
+        u64* err[4];
+        for (int l = 0; l < 4; ++l) c[l] = coefs(m + l), err[l] = R.err + size_t(m + l) * kSlotsPerLayer;
+        launch_tbn<T>(4, tb_rows_, tb_waves_, cfg_.fma, m == 1, A, B, R.g[lvl(m + 2)], R.g[lvl(m + 3)], R.gv, boxes,
+                      nbox, R.cdom, R.error.i0, R.error.i1, R.wrap3, R.wrap4, sp, R.txy, R.tz, R.rtxy, R.rtz, c,
+                      err, cfg_.chunk, s);
+    }
+
+    // the seam pre-kernels of the sweep that starts at layer m (span 3 or 4); `in`: into the
+    // interior's own scratch copy (overlapped self-wrap runs: the interior and the shells run
+    // concurrently on two streams)
+    void seam_pre(DevRank<T>& R, int m, int span, hipStream_t s, bool in = false) {
+        SeamScratch use(R, in);
+        if (span == 4) seam4(R, m, s);
+        else seam_c(R, m, s);
+    }
+    void sweep_deep(DevRank<T>& R, int m, int span, hipStream_t s, const Box* boxes = nullptr, int nbox = 0,
+                    bool in = false) {
+        SeamScratch use(R, in);
+        if (span == 4) sweep4(R, m, s, boxes, nbox);
+        else sweep3(R, m, s, boxes, nbox);
+    }
+    // selects the seam scratch set for the calls in its scope
+    struct SeamScratch {
+        DevRank<T>& R;
+        T* saved;
+        SeamScratch(DevRank<T>& r, bool in) : R(r), saved(r.seamc_buf) {
+            if (in && r.seamc_in) r.seamc_buf = r.seamc_in;
+        }
+        ~SeamScratch() { R.seamc_buf = saved; }
+    };
+
     void sweep3(DevRank<T>& R, int m, hipStream_t s, const Box* boxes = nullptr, int nbox = 0) {
         const T* A = R.g[lvl(m - 1)];
         const T* B = R.g[lvl(m - 2)];
         const SeamPartners<T> sp = seam_partners(R, m, nullptr);
         if (!boxes) boxes = &R.compute, nbox = 1;
+        if (tbn_ && tbd_ == 3) {  // the depth-generic kernel at depth 3 (A/B against k_tb3)
+            TbnSeam<T> ts;
+            ts.next_i = sp.next_i, ts.prev_i = sp.prev_i;
+            ts.nP[0] = sp.nA, ts.nP[1] = sp.nC, ts.pP[0] = sp.pA, ts.pP[1] = sp.pC;
+            StepCoefs c[3];
+            u64* err[3];
+            for (int l = 0; l < 3; ++l) c[l] = coefs(m + l), err[l] = R.err + size_t(m + l) * kSlotsPerLayer;
+            launch_tbn<T>(3, tb_rows_, tb_waves_, cfg_.fma, m == 1, A, B, R.g[lvl(m + 1)], R.g[lvl(m + 2)], R.gv,
+                          boxes, nbox, R.cdom, R.error.i0, R.error.i1, R.wrap2, R.wrap3, ts, R.txy, R.tz, R.rtxy,
+                          R.rtz, c, err, cfg_.chunk, s);
+            return;
+        }
         launch_tb3<T>(tb_rows_, tb_waves_, cfg_.delta, cfg_.fma, m == 1, A, B, R.g[lvl(m + 1)], R.g[lvl(m + 2)], R.gv, boxes,
                       nbox, R.cdom, R.error.i0, R.error.i1, R.wrap2, R.wrap3, sp, R.txy, R.tz, R.rtxy, R.rtz,
                       coefs(m), coefs(m + 1), coefs(m + 2), R.err + size_t(m) * kSlotsPerLayer,
@@ -1155,7 +1293,7 @@ private:
     void inject_after_exchange(DevRank<T>& R, int n, hipStream_t s) {
         if (selftest_) return;
         // exchanges follow every sweep: a fault layer inside the sweep hits its exchange
-        const int lo = tbd_ == 3 ? n - 3 : (tb_ ? n - 2 : n - 1);
+        const int lo = tb_ ? n - tbd_ : n - 1;
         if (fault_.kind == "drop_face" && fault_.hits_range(R.topo.rank, lo, n))
             HIP_CHECK(hipMemsetAsync(plane(R, lvl(n), 0), 0, R.gv.si * sizeof(T), s));
     }
@@ -1190,6 +1328,12 @@ private:
             return;
         }
         mark(s, 6);
+        {
+            std::map<std::pair<int, int>, size_t> link;
+            for (auto& S : ranks_)
+                for (auto& f : S.plan.sends) link[{S.topo.rank, f.peer}] += size_t(f.count) * sizeof(T);
+            model_link(link, s);
+        }
         for (auto& S : ranks_)
             for (size_t m = 0; m < S.plan.sends.size(); ++m) {
                 const auto& f = S.plan.sends[m];
@@ -1212,6 +1356,20 @@ private:
             pack_faces(R, n, s, false);
             inject_after_exchange(R, n, s);
         }
+    }
+
+    // --model-link: the loopback transfer of one exchange round also waits the time the
+    // busiest link of the round needs — every (sender, receiver) pair has its own xGMI link on a
+    // fully connected node and every rank sends at once, so a round lasts max over pairs of
+    // bytes / bandwidth, plus one latency. One wave spins that long on the exchange stream (one
+    // CU, as a remote transfer's kernels), so overlap experiments on one GPU see a halo that
+    // costs wall time without costing the interior sweep its CUs.
+    void model_link(const std::map<std::pair<int, int>, size_t>& link_bytes, hipStream_t s) {
+        if (cfg_.model_link_gbps <= 0) return;
+        size_t most = 0;
+        for (const auto& kv : link_bytes) most = std::max(most, kv.second);
+        const double sec = double(most) / (cfg_.model_link_gbps * 1e9) + cfg_.model_link_lat_us * 1e-6;
+        launch_spin(u64(sec * clock_khz_ * 1e3), s);
     }
 
     // ---- loopback copies and the RCCL mirror ------------------------------------------------
@@ -1610,26 +1768,37 @@ private:
             // never store to them; a tb3 C layer is not stored)
             for (int q = n; q < n + span; ++q)
                 for (auto& R : ranks_)
-                    if ((first_write_[q + 1] || q == start) && !(span == 3 && q == n))
+                    if ((first_write_[q + 1] || q == start) && !(span >= 3 && q < n + span - 2))
                         launch_zero_faces<T>(R.g[lvl(q)], R.gv, R.zero_mask, s_comp_);
-            if (span == 3 && overlap_) {
+            if (span >= 3 && overlap_) {
+                // Shells on the (high-priority) comm stream right behind the previous halo,
+                // concurrently with the interior on the compute stream, as the two-layer path:
+                // the shells need that halo and the previous sweep's interior; the interior reads
+                // only owned nodes of the previous sweep (it stays `span` nodes away from every
+                // remote ghost), so it never waits for a halo. The next exchange follows the
+                // shells on the comm stream; the compute stream waits for the shells before the
+                // next interior (whose rings reach into them).
+                HIP_CHECK(hipEventRecord(ev_layer_, s_comp_));
+                HIP_CHECK(hipStreamWaitEvent(s_comm_, ev_layer_, 0));
+                for (auto& R : ranks_) {
+                    seam_pre(R, n, span, s_comm_);
+                    if (!R.tb_shell.empty())
+                        sweep_deep(R, n, span, s_comm_, R.tb_shell.data(), int(R.tb_shell.size()));
+                }
+                HIP_CHECK(hipEventRecord(ev_shell_, s_comm_));
                 for (auto& R : ranks_) {
                     // periodic self-wrap: the interior spans every x plane, so it reads the seam
-                    // C planes too (at positions that need no remote halo); evaluated again
-                    // after the halo for the shell
-                    if (R.plan.self_x && !R.tb_interior.empty()) seam_c(R, n, s_comp_);
-                    if (!R.tb_interior.empty()) sweep3(R, n, s_comp_, &R.tb_interior, 1);
+                    // partner planes too (at positions that need no remote halo) — from its own
+                    // copy, the shells' copy is rewritten concurrently on the comm stream
+                    if (R.plan.self_x && !R.tb_interior.empty()) seam_pre(R, n, span, s_comp_, true);
+                    if (!R.tb_interior.empty()) sweep_deep(R, n, span, s_comp_, &R.tb_interior, 1, true);
                 }
-                HIP_CHECK(hipStreamWaitEvent(s_comp_, ev_halo_, 0));
+                HIP_CHECK(hipStreamWaitEvent(s_comp_, ev_shell_, 0));
+                comm_follows = true;
+            } else if (span >= 3) {
                 for (auto& R : ranks_) {
-                    seam_c(R, n, s_comp_);
-                    if (!R.tb_shell.empty())
-                        sweep3(R, n, s_comp_, R.tb_shell.data(), int(R.tb_shell.size()));
-                }
-            } else if (span == 3) {
-                for (auto& R : ranks_) {
-                    seam_c(R, n, s_comp_);
-                    sweep3(R, n, s_comp_);
+                    seam_pre(R, n, span, s_comp_);
+                    sweep_deep(R, n, span, s_comp_);
                 }
             } else if (span == 2 && overlap_) {
                 // Shells on the (high-priority) comm stream right behind the previous halo,
@@ -1670,9 +1839,11 @@ private:
             } else {
                 for (auto& R : ranks_) step_boxes(R, n, &R.compute, 1, kind_, s_comp_);
             }
-            for (int q = n; q < n + span; ++q)
-                for (auto& R : ranks_)  // tb3 never stores C = u^n: a fault there goes to u^{n+1}
-                    if (!(span == 3 && q == n)) inject_after_compute(R, q, s_comp_, q == n + 1 && span == 3 ? n : q);
+            // deep sweeps never store their first span-2 layers: a fault there goes to the first
+            // stored layer
+            const int first_stored = span >= 3 ? n + span - 2 : n;
+            for (int q = first_stored; q < n + span; ++q)
+                for (auto& R : ranks_) inject_after_compute(R, q, s_comp_, q == first_stored ? n : q);
             mark(s_comp_, 1);
             const int last = n + span - 1;
             if (last < K) issue_exchange(last, comm_follows);
@@ -1978,7 +2149,8 @@ private:
     int tb_waves_ = 4;
     int tb_occ_ = 0;
     int tb_nwk_ = 1;    // tb2 waves along k (tile width 64 * tb_nwk_)
-    int tbd_ = 1;       // layers per sweep (1, 2 or 3)
+    int tbd_ = 1;       // layers per sweep (1, 2, 3 or 4)
+    bool tbn_ = false;  // deep sweeps through k_tbn (tb4; "tbn3": the depth-generic kernel at 3)
     hipGraphExec_t gexec_ = nullptr;  // captured IC + time loop (graph_eligible())
     bool graph_failed_ = false;
     int G_ = 1;         // ghost depth

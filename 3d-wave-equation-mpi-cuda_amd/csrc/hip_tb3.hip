@@ -644,7 +644,7 @@ struct SeamCOp {
 };
 template <class T>
 struct SeamCParams {
-    SeamCOp<T> op[2];
+    SeamCOp<T> op[kMaxSeamOps];
     int sj, jmin, jmax, kmin, kmax;
     int cj0, cj1, ck0, ck1;
     T hx2, hy2, hz2, yx2, yy2, yz2, coef;
@@ -820,7 +820,7 @@ void launch_tb3(int rows, int waves, bool delta, bool fm, bool first, const T* A
 template <class T>
 void launch_seam_c(bool first, bool delta, bool fm, const SeamCPlane<T>* ops, int nops, const GridView& gv,
                    const Box& cdom, const StepCoefs& cC, hipStream_t s) {
-    W3D_REQUIRE(nops >= 0 && nops <= 2, "seam C: at most two planes");
+    W3D_REQUIRE(nops >= 0 && nops <= kMaxSeamOps, "seam C: too many planes");
     if (nops == 0) return;
     SeamCParams<T> p{};
     for (int q = 0; q < nops; ++q)

@@ -1,0 +1,686 @@
+// Deep temporal blocking: D leapfrog layers per sweep (TBN, D = 3 or 4) on CDNA4.
+//
+// One sweep reads A = u^{m-1} and B = u^{m-2} and writes only the last two layers
+// U_{D-2} = u^{m+D-2} and U_{D-1} = u^{m+D-1} (the next sweep's B and A); the layers before them
+// live in registers and LDS (their errors are still reduced). HBM traffic is 32 B per node per
+// D layers: 10.7 B per layer at D = 3 (hip_tb3.hip), 8 B at D = 4 — against 24 for one layer
+// per pass (the reference's loop, mpi_new.cpp:335-347 / cuda_sol_kernels.cu:24-47).
+//
+// Workgroup = NW wave64s owning a (NW*R rows) x 64 tile of U_{D-1} that marches along i. Layer
+// l is evaluated l planes behind layer 0, on a (D-1-l)-node ring around the tile (redundantly
+// with the neighbour tiles; identical operations, so bitwise equal):
+//   iteration i:  stage A(i) (tile + D-ring) -> barrier
+//                 U_0(i)       on tile + (D-1)-ring  from A(i-1..i+1), B(i)
+//                 U_l(i - l)   on tile + (D-1-l)-ring from U_{l-1} (staged last iteration) and
+//                              U_{l-2} (A for l = 1) of the same plane
+// Every staged tile is double-buffered, so one barrier per plane. Register state sits in slots
+// indexed by plane number mod 4 / mod 2 with the i loop unrolled by 4 (no copies of in-flight
+// loads): U_l(x) lives in slot (x + l - i0) & 3, i.e. the phase of the iteration that made it.
+//
+// Ring ownership (as k_tb3): every ring node belongs to ONE thread — rings 1..D-1 whole, ring D
+// (A only) without its corners, which no in-plane 5-point stencil of layer 0 reads — RP
+// positions per thread. A slot whose first possible ring is r only carries the history of the
+// layers evaluated on ring r (compile-time), so the far rings cost registers for A and B only.
+//
+// Load pipeline depth (DEEP bits): bit 0 — A is prefetched three planes ahead instead of two: A(i-1)
+// is read from the LDS tile staged last iteration (still intact until the next barrier), so its
+// register slot takes A(i+3) at the top of the iteration; bit 1 — B two planes ahead (4 slots).
+//
+// Periodic seam (the reference keeps both x = 0 and x = N, mpi_new.cpp:170-176): at plane an_i
+// (the ghost copy of global N-1) the x+ neighbour of layer l is the partner plane nP[l] — A at
+// x = N for layer 0, U_{l-1} evaluated there (launch_seam_c, before the sweep) for l >= 1 —
+// and mirrored at ap_i; separate, rarely taken instantiation of the plane body.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <climits>
+#include <cstdlib>
+#include <cmath>
+#include <type_traits>
+#include <utility>
+
+#include "device_common.hpp"
+
+namespace wave3d {
+namespace {
+
+template <class F, int... I>
+__device__ __forceinline__ void sfor_impl(F&& f, std::integer_sequence<int, I...>) {
+    (f(std::integral_constant<int, I>{}), ...);
+}
+// f(integral_constant<0>) .. f(integral_constant<N-1>), unrolled at compile time
+template <int N, class F>
+__device__ __forceinline__ void sfor(F&& f) {
+    sfor_impl(f, std::make_integer_sequence<int, N>{});
+}
+template <int V>
+using Ic = std::integral_constant<int, V>;
+
+template <class T>
+struct TbnParams {
+    // level bases pre-biased on the host: plane i's block starts at base + (i + pbias) * pbytes
+    const char* A;
+    const char* B;
+    char* O[2];  // U_{D-2}, U_{D-1}
+    unsigned pbytes;
+    int pbias;
+    int order;  // tile order (tile_order(), as k_tb3)
+    int sj;
+    int poff;
+    int jmin, jmax, kmin, kmax;  // storage bounds (logical)
+    int cj0, cj1, ck0, ck1;      // stencil-valued region (0 outside: Dirichlet)
+    int nbox;
+    BoxLaunch box[kMaxBoxes];
+    int ei0, ei1;
+    int w_lo[2][2], w_hi[2][2], w_sh[2][2];  // self-wrap of O[0] (depth D-1) and O[1] (depth D)
+    int an_i, ap_i;
+    const T* nP[kTbnMaxDepth - 1];  // x+ partners at an_i: A, then U_0 .. U_{D-3} (logical planes)
+    const T* pP[kTbnMaxDepth - 1];  // x- partners at ap_i
+    const T* txy;  // sx*sy rows (launch_txy)
+    int tpj;
+    const T* tz;
+    const T* txr;  // --math fma: (sx sy, 1/|sx sy|) pairs and 1/|tz|
+    const T* rtz;
+    T hx2, hy2, hz2, yx2, yy2, yz2;
+    T coef[kTbnMaxDepth], ct[kTbnMaxDepth];
+    T fc[2][3];  // --math fma: coef/h^2 per axis of layer 0 (fc[0]) and of every later layer
+    T ict[kTbnMaxDepth];
+    u64* err[kTbnMaxDepth];
+};
+
+// Tile geometry of a D-layer sweep over TJ x 64 tiles (coordinates in the "A frame": row y =
+// j - jt + D, column x = k - kb + D).
+template <int D, int TJ>
+struct TbnGeom {
+    // staged layer s: 0 = A (ring D), s >= 1 = U_{s-1} (ring D - s); frame origin (s, s)
+    static constexpr int H(int s) { return TJ + 2 * (D - s); }
+    static constexpr int W(int s) { return kTK + 2 * (D - s); }
+    static constexpr int size(int s) { return H(s) * W(s); }
+    static constexpr int off(int s) { return s == 0 ? 0 : off(s - 1) + 2 * size(s - 1); }
+    static constexpr int total = off(D);
+    // ring r positions: rings 1..D-1 whole, ring D without corners
+    static constexpr int npos(int r) { return 2 * (kTK + 2 * (r - 1)) + 2 * (TJ + 2 * (r - (r == D ? 1 : 0))); }
+    static constexpr int first(int r) { return r <= 1 ? 0 : first(r - 1) + npos(r - 1); }
+    static constexpr int nall = first(D + 1);
+    // ring of ring position q (D + 1: none)
+    static constexpr int ring_of(int q) {
+        int r = 1;
+        while (r <= D && q >= first(r + 1)) ++r;
+        return r;
+    }
+};
+
+template <class T, int D, bool FIRST, int R, int NW, bool FM, int DEEP>
+__global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(1, 8))) k_tbn(const TbnParams<T> p) {
+    constexpr bool ADEEP = DEEP & 1;      // A(i+3) into the slot of A(i-1) (read from LDS)
+    constexpr int NB = DEEP & 2 ? 4 : 2;  // B slots: B(i + NB/2) prefetched at iteration i
+    constexpr int ADIST = ADEEP ? 3 : 2, BDIST = NB / 2;
+    constexpr int TJ = NW * R;
+    using Gm = TbnGeom<D, TJ>;
+    constexpr int NT = NW * 64;
+    constexpr int RP = (Gm::nall + NT - 1) / NT;  // ring positions per thread
+    constexpr unsigned ES = sizeof(T);
+    constexpr int NU = D - 1;                // own history: U_0 .. U_{D-2}
+    constexpr int NRU = D >= 3 ? D - 2 : 1;  // ring history: U_0 .. U_{D-3}
+    __shared__ T lds[Gm::total];
+    // staged layer s, buffer h, A-frame coordinates (y, x)
+    auto L = [&](auto sc, auto hc, int y, int x) -> T& {
+        constexpr int s = decltype(sc)::value, h = decltype(hc)::value;
+        return lds[Gm::off(s) + h * Gm::size(s) + (y - s) * Gm::W(s) + (x - s)];
+    };
+
+    const int bid = blockIdx.x;
+    const int b = find_box(p, bid);
+    const BoxLaunch Bx = p.box[b];
+    int local = bid - Bx.block_begin;
+    int tk, tj;
+    if (p.order == 2 && Bx.tiles_j % kXcds == 0) {
+        // XCD x = id mod 8 runs tile rows [x*hb, x*hb + hb) of every k-tile and chunk
+        const int hb = Bx.tiles_j / kXcds, x = local % kXcds;
+        local /= kXcds;
+        tj = x * hb + local % hb;
+        local /= hb;
+        tk = local % Bx.tiles_k;
+        local /= Bx.tiles_k;
+    } else if (p.order) {
+        tj = local % Bx.tiles_j;
+        local /= Bx.tiles_j;
+        tk = local % Bx.tiles_k;
+        local /= Bx.tiles_k;
+    } else {
+        tk = local % Bx.tiles_k;
+        local /= Bx.tiles_k;
+        tj = local % Bx.tiles_j;
+        local /= Bx.tiles_j;
+    }
+    const int ci = local;
+    const int kb = Bx.kbase + tk * kTK;
+    const int jt = Bx.j0 + tj * TJ;
+    const int ib = Bx.i0 + ci * Bx.chunk;
+    const int ie = min(Bx.i1, ib + Bx.chunk - 1);
+    const int i0 = ib - (D - 1);  // first iteration (layer 0 of plane i0)
+    const int lane = threadIdx.x & 63;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int sj = p.sj;
+    const unsigned pbytes = p.pbytes;
+
+    auto inb = [&](int j, int k) { return j >= p.jmin && j <= p.jmax && k >= p.kmin && k <= p.kmax; };
+    auto incd = [&](int j, int k) { return j >= p.cj0 && j <= p.cj1 && k >= p.ck0 && k <= p.ck1; };
+    auto boff = [&](int j, int k, bool ok) { return ok ? unsigned(j * sj + k + p.poff) * ES : kOOB; };
+    auto prs = [&](const char* base, int i, unsigned nb) {
+        return plane_rsrc(base + u64(unsigned(i + p.pbias)) * pbytes, nb);
+    };
+    auto lrs = [&](const T* plane) { return plane_rsrc(plane - p.poff, pbytes); };
+
+    // ---- own nodes ------------------------------------------------------------------------
+    const int k = kb + lane;
+    unsigned oa[R], ob[R], os[R];
+    bool ovalid[R], ocd[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const int j = jt + w * R + r;
+        ocd[r] = incd(j, k);
+        ovalid[r] = k >= Bx.k0 && k <= Bx.k1 && j <= Bx.j1;
+        oa[r] = boff(j, k, inb(j, k));
+        ob[r] = boff(j, k, !FIRST && inb(j, k) && ocd[r]);
+        os[r] = boff(j, k, ovalid[r]);
+    }
+    const T otz = (k >= Bx.k0 && k <= Bx.k1) ? p.tz[k] : T(0);
+    const T ortz = FM && k >= Bx.k0 && k <= Bx.k1 ? p.rtz[k] : T(0);
+    const T* const txw = p.txy + (jt + w * R);
+    T om[R];  // --math fma: 1 on valid own nodes, 0 on masked lanes (branch-free errors)
+#pragma unroll
+    for (int r = 0; r < R; ++r) om[r] = ovalid[r] ? T(1) : T(0);
+    // self-wrap ranges of O[0] / O[1] met by this work item (wave-uniform bits)
+    int rare = 0;
+#pragma unroll
+    for (int g = 0; g < 2; ++g) {
+        if (p.w_lo[0][g] <= ie && p.w_hi[0][g] >= ib) rare |= 1;
+        if (p.w_lo[1][g] <= ie && p.w_hi[1][g] >= ib) rare |= 2;
+    }
+    rare = __builtin_amdgcn_readfirstlane(rare);
+    // steady-state window [flo, fhi]: every layer on an own-range plane, prefetch live, off the
+    // periodic seam and the self-wrap planes (those sit at the ends of the x range, so each one
+    // trims the window from its nearer end)
+    int flo = ib + D - 1, fhi = min(ie + D - ADIST, ie + D - 1 - BDIST);
+    auto cut = [&](int lo, int hi) {
+        if (lo > hi || hi < flo || lo > fhi) return;
+        if (lo - flo <= fhi - hi) flo = hi + 1;
+        else fhi = lo - 1;
+    };
+    cut(p.an_i, p.an_i + D - 2);
+    cut(p.ap_i, p.ap_i + D - 2);
+#pragma unroll
+    for (int g = 0; g < 2; ++g) {
+        cut(p.w_lo[0][g] + D - 2, p.w_hi[0][g] + D - 2);
+        cut(p.w_lo[1][g] + D - 1, p.w_hi[1][g] + D - 1);
+    }
+    flo = __builtin_amdgcn_readfirstlane(flo);
+    fhi = __builtin_amdgcn_readfirstlane(fhi);
+
+    // ---- ring positions of this thread ------------------------------------------------------
+    // d-ring = rows jt-d / jt+TJ-1+d over cols kb-d+1 .. kb+64+d-2, then cols kb-d / kb+63+d over
+    // rows jt-d+c .. jt+TJ-1+d-c (c = 1 drops the corners)
+    auto ring = [&](int d, int c, int idx, int& rj, int& rk) {
+        const int wd = kTK + 2 * (d - 1), hd = TJ + 2 * (d - c);
+        if (idx < wd) rj = jt - d, rk = kb - (d - 1) + idx;
+        else if (idx < 2 * wd) rj = jt + TJ - 1 + d, rk = kb - (d - 1) + idx - wd;
+        else if (idx < 2 * wd + hd) rj = jt - d + c + (idx - 2 * wd), rk = kb - d;
+        else rj = jt - d + c + (idx - 2 * wd - hd), rk = kb + kTK - 1 + d;
+    };
+    int rg[RP], ry[RP], rx[RP];       // ring (0: none) and A-frame coordinates
+    unsigned ra_off[RP], rb_off[RP];  // A / B load offsets (kOOB when masked)
+    bool rcd[RP];                     // stencil-valued node (else 0: Dirichlet face)
+#pragma unroll
+    for (int s = 0; s < RP; ++s) {
+        const int q = threadIdx.x + s * NT;
+        int g = 0, rj = jt, rk = kb;
+#pragma unroll
+        for (int d = 1; d <= D; ++d)
+            if (g == 0 && q < Gm::first(d + 1)) g = d, ring(d, d == D ? 1 : 0, q - Gm::first(d), rj, rk);
+        rg[s] = g;
+        ry[s] = rj - jt + D, rx[s] = rk - kb + D;
+        rcd[s] = g != 0 && g < D && incd(rj, rk);
+        ra_off[s] = boff(rj, rk, g != 0 && inb(rj, rk));
+        rb_off[s] = boff(rj, rk, !FIRST && rcd[s] && inb(rj, rk));
+    }
+
+    // slots (iteration i = i0 + q, phase P = q & 3): A(x) (x - i0 + 1) & 3 -> A(i-1) = P,
+    // A(i) = P+1, A(i+1) = P+2, A(i+2) = P+3; B(x) (x - i0) & 1; U_l(x) (x + l - i0) & 3 ->
+    // U_l of this iteration in P, of the last in P+3, of the one before in P+2
+    T a[4][R], bb[NB][R], u[NU][4][R];
+    T ra[RP][4], rb[RP][NB], ru[RP][NRU][4];
+    {
+        const auto rAm = prs(p.A, i0 - 1, pbytes), rA0 = prs(p.A, i0, pbytes), rA1 = prs(p.A, i0 + 1, pbytes);
+        const auto rA2 = prs(p.A, i0 + 2, ADEEP ? pbytes : 0u);  // ADEEP: A(i0+2) in the prologue too
+        const auto rB = prs(p.B, i0, pbytes), rB1 = prs(p.B, i0 + 1, NB == 4 ? pbytes : 0u);
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            a[0][r] = bld<T>(rAm, oa[r]);
+            a[1][r] = bld<T>(rA0, oa[r]);
+            a[2][r] = bld<T>(rA1, oa[r]);
+            a[3][r] = ADEEP ? bld<T>(rA2, oa[r]) : T(0);
+            bb[0][r] = bld<T>(rB, ob[r]);
+#pragma unroll
+            for (int t = 1; t < NB; ++t) bb[t][r] = t == 1 && NB == 4 ? bld<T>(rB1, ob[r]) : T(0);
+#pragma unroll
+            for (int l = 0; l < NU; ++l)
+#pragma unroll
+                for (int t = 0; t < 4; ++t) u[l][t][r] = T(0);
+        }
+#pragma unroll
+        for (int s = 0; s < RP; ++s) {
+            ra[s][0] = bld<T>(rAm, ra_off[s]);
+            ra[s][1] = bld<T>(rA0, ra_off[s]);
+            ra[s][2] = bld<T>(rA1, ra_off[s]);
+            ra[s][3] = ADEEP ? bld<T>(rA2, ra_off[s]) : T(0);
+            rb[s][0] = bld<T>(rB, rb_off[s]);
+#pragma unroll
+            for (int t = 1; t < NB; ++t) rb[s][t] = t == 1 && NB == 4 ? bld<T>(rB1, rb_off[s]) : T(0);
+#pragma unroll
+            for (int l = 0; l < NRU; ++l)
+#pragma unroll
+                for (int t = 0; t < 4; ++t) ru[s][l][t] = T(0);
+        }
+        if constexpr (ADEEP) {  // A(i0-1) is read from the tile "staged last iteration" (buffer 1)
+#pragma unroll
+            for (int r = 0; r < R; ++r) L(Ic<0>{}, Ic<1>{}, D + w * R + r, D + lane) = a[0][r];
+#pragma unroll
+            for (int s = 0; s < RP; ++s)
+                if (rg[s]) L(Ic<0>{}, Ic<1>{}, ry[s], rx[s]) = ra[s][0];
+        }
+    }
+
+    using Rel = std::conditional_t<FM, RelMax<T>, RelArg<T>>;  // fma: |d| * 1/|f| max
+    T ma[D], chk[D];
+    Rel mr[D];
+#pragma unroll
+    for (int l = 0; l < D; ++l) ma[l] = T(kErrInit), chk[l] = T(0);
+
+    // layer-l arithmetic: lap() = Laplacian (exact) or coef*Laplacian (FM); upd() = the
+    // Taylor start (layer 0 of the first sweep) or the leapfrog from it
+    auto lap = [&](auto lc, T ctr, T xm, T xp, T ym, T yp, T zm, T zp) {
+        constexpr int l = decltype(lc)::value;
+        if constexpr (FM) {
+            constexpr int f = FIRST && l == 0 ? 0 : 1;
+            return coef_lap_fma(ctr, xm, xp, ym, yp, zm, zp, p.fc[f][0], p.fc[f][1], p.fc[f][2]);
+        } else {
+            return laplace7_cr(ctr, xm, xp, ym, yp, zm, zp, p.hx2, p.hy2, p.hz2, p.yx2, p.yy2, p.yz2);
+        }
+    };
+    auto upd = [&](auto lc, T ctr, T pw, T l_) {
+        constexpr int l = decltype(lc)::value;
+        if constexpr (FM) {
+            if constexpr (FIRST && l == 0) return ctr + l_;
+            else return leapfrog_fma(ctr, pw, l_);
+        } else {
+            if constexpr (FIRST && l == 0) return taylor_first(ctr, l_, p.coef[0]);
+            else return leapfrog(ctr, pw, l_, p.coef[l]);
+        }
+    };
+
+    // Errors of every layer are taken at plane i - (D-1), when all D values of that plane are
+    // in registers: one analytic-table row per plane (f = ((sx sy) sz) ct per layer, stencil_math
+    // analytic()), loaded an iteration ahead into a plane-parity slot (a scalar load). --math fma:
+    // the (sx sy, 1/|sx sy|) pair (txr); exact: sx sy (txy).
+    constexpr int NQ = FM ? 2 : 1;
+    T tq[2][R][NQ];
+    auto load_row = [&](auto slotc, int q) {  // slot as a constant: tq stays in registers
+        constexpr int slot = decltype(slotc)::value;
+        q = min(max(q, ib), ie);
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            if constexpr (FM) {
+                const T* const tr = p.txr + 2 * (q * p.tpj + (jt + w * R));
+                tq[slot][r][0] = ldconst(tr, 2 * r);
+                tq[slot][r][1] = ldconst(tr, 2 * r + 1);
+            } else {
+                tq[slot][r][0] = ldconst(txw + q * p.tpj, r);
+            }
+        }
+    };
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+#pragma unroll
+        for (int n = 0; n < NQ; ++n) tq[0][r][n] = tq[1][r][n] = T(0);
+
+    auto plane = [&](auto phase, auto alias, const int i) {
+        constexpr int P = decltype(phase)::value;
+        constexpr bool ALIAS = decltype(alias)::value;
+        constexpr bool FAST = !ALIAS;
+        constexpr int S0 = P & 3, S1 = (P + 1) & 3, S2 = (P + 2) & 3, S3 = (P + 3) & 3;
+        constexpr int H0 = P & 1, H1 = (P + 1) & 1;
+        constexpr int SA = ADEEP ? S0 : S3;                           // slot of the A prefetch
+        constexpr int BC = P & (NB - 1), BP = (P + BDIST) & (NB - 1);  // B(i), B prefetch slots
+
+        // ---- prefetch A(i+ADIST), B(i+BDIST) (own and ring; 0-record descriptors when done) --
+        {
+            const bool moreA = FAST || i + ADIST <= ie + D, moreB = FAST || i + BDIST <= ie + D - 1;
+            const auto rAn = prs(p.A, i + (moreA ? ADIST : 0), moreA ? pbytes : 0u);
+            const auto rBn = prs(p.B, i + (moreB ? BDIST : 0), moreB ? pbytes : 0u);
+            // ADEEP: A(i-1) of the own nodes is read from LDS below; the ring's too
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                a[SA][r] = bld<T>(rAn, oa[r]);
+                bb[BP][r] = bld<T>(rBn, ob[r]);
+            }
+#pragma unroll
+            for (int s = 0; s < RP; ++s) {
+                ra[s][SA] = bld<T>(rAn, ra_off[s]);
+                rb[s][BP] = bld<T>(rBn, rb_off[s]);
+            }
+        }
+        // ---- stage A(i) --------------------------------------------------------------------
+#pragma unroll
+        for (int r = 0; r < R; ++r) L(Ic<0>{}, Ic<H0>{}, D + w * R + r, D + lane) = a[S1][r];
+#pragma unroll
+        for (int s = 0; s < RP; ++s)
+            if (rg[s]) L(Ic<0>{}, Ic<H0>{}, ry[s], rx[s]) = ra[s][S1];
+        __syncthreads();
+
+        T ev[R];  // U_{D-1}(i - D + 1): stored and its errors taken below
+#pragma unroll
+        for (int r = 0; r < R; ++r) ev[r] = T(0);
+        sfor<D>([&](auto lc) {
+            constexpr int l = decltype(lc)::value;
+            constexpr int HS = l == 0 ? H0 : H1;  // buffer of the staged layer read (A: this iteration)
+            const int x = i - l;
+            if (!(FAST || (x >= ib - (D - 1 - l) && x <= ie + (D - 1 - l)))) return;
+            // ---- own nodes ----
+            T v[R];
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                const int y = D + w * R + r, xx = D + lane;
+                T ctr, xm, xp, pw;
+                // A(i-1): its register (ADEEP: taken by the prefetch) or the tile staged last iteration
+                auto am1 = [&]() { return ADEEP ? L(Ic<0>{}, Ic<H1>{}, y, xx) : a[S0][r]; };
+                if constexpr (l == 0) {
+                    ctr = a[S1][r], xm = am1(), xp = a[S2][r], pw = bb[BC][r];
+                } else {
+                    ctr = u[l - 1][S3][r], xp = u[l - 1][S0][r], xm = u[l - 1][S2][r];
+                    if constexpr (l == 1) pw = am1();
+                    else pw = u[l - 2][S2][r];
+                }
+                if constexpr (ALIAS && l <= D - 2) {
+                    if (x == p.an_i) xp = bld<T>(lrs(p.nP[l]), oa[r]);
+                    if (x == p.ap_i) xm = bld<T>(lrs(p.pP[l]), oa[r]);
+                }
+                const T lp = lap(lc, ctr, xm, xp, L(lc, Ic<HS>{}, y - 1, xx), L(lc, Ic<HS>{}, y + 1, xx),
+                                 L(lc, Ic<HS>{}, y, xx - 1), L(lc, Ic<HS>{}, y, xx + 1));
+                v[r] = ocd[r] ? upd(lc, ctr, pw, lp) : T(0);
+                if constexpr (l <= D - 2) {
+                    u[l][S0][r] = v[r];
+                    L(Ic<l + 1>{}, Ic<H0>{}, y, xx) = v[r];
+                }
+            }
+            // ---- ring nodes (rings 1 .. D-1-l) ----
+            if constexpr (l <= D - 2) {
+                sfor<RP>([&](auto sc) {
+                    constexpr int s = decltype(sc)::value;
+                    if constexpr (Gm::ring_of(s * NT) <= D - 1 - l) {
+                        if (rg[s] >= 1 && rg[s] <= D - 1 - l) {
+                            T ctr, xm, xp, pw;
+                            auto am1 = [&]() { return ADEEP ? L(Ic<0>{}, Ic<H1>{}, ry[s], rx[s]) : ra[s][S0]; };
+                            if constexpr (l == 0) {
+                                ctr = ra[s][S1], xm = am1(), xp = ra[s][S2], pw = rb[s][BC];
+                            } else {
+                                ctr = ru[s][l - 1][S3], xp = ru[s][l - 1][S0], xm = ru[s][l - 1][S2];
+                                if constexpr (l == 1) pw = am1();
+                                else pw = ru[s][l - 2][S2];
+                            }
+                            if constexpr (ALIAS) {
+                                if (x == p.an_i) xp = bld<T>(lrs(p.nP[l]), ra_off[s]);
+                                if (x == p.ap_i) xm = bld<T>(lrs(p.pP[l]), ra_off[s]);
+                            }
+                            const int y = ry[s], xx = rx[s];
+                            const T lp = lap(lc, ctr, xm, xp, L(lc, Ic<HS>{}, y - 1, xx), L(lc, Ic<HS>{}, y + 1, xx),
+                                             L(lc, Ic<HS>{}, y, xx - 1), L(lc, Ic<HS>{}, y, xx + 1));
+                            const T cv = rcd[s] ? upd(lc, ctr, pw, lp) : T(0);
+                            if constexpr (l <= D - 3) ru[s][l][S0] = cv;
+                            L(Ic<l + 1>{}, Ic<H0>{}, y, xx) = cv;
+                        }
+                    }
+                });
+            }
+            // ---- stores of the last two layers (own planes, + periodic self-wrap) ----
+            if constexpr (l >= D - 2) {
+                constexpr int o = l - (D - 2);
+                if (FAST || (x >= ib && x <= ie)) {
+                    const auto rd = prs(p.O[o], x, pbytes);
+#pragma unroll
+                    for (int r = 0; r < R; ++r) bst<2>(v[r], rd, os[r]);
+                    if (!FAST && (rare & (1 << o))) {
+#pragma unroll
+                        for (int g = 0; g < 2; ++g)
+                            if (x >= p.w_lo[o][g] && x <= p.w_hi[o][g]) {
+                                const auto rw = prs(p.O[o], x + p.w_sh[o][g], pbytes);
+#pragma unroll
+                                for (int r = 0; r < R; ++r) bst<2>(v[r], rw, os[r]);
+                            }
+                    }
+                }
+            }
+            if constexpr (l == D - 1) {
+#pragma unroll
+                for (int r = 0; r < R; ++r) ev[r] = v[r];
+            }
+        });
+
+        // ---- errors of plane e = i - (D-1), every layer ----------------------------------------
+        const int e = i - (D - 1);
+        if (FAST || (e >= ib && e <= ie)) {
+            constexpr int HE = (P + 4 - (D - 1)) & 1;  // table row slot of plane e
+            const bool eplane = e >= p.ei0 && e <= p.ei1;
+            T fb[R];
+#pragma unroll
+            for (int r = 0; r < R; ++r) fb[r] = tq[HE][r][0] * otz;  // (sx sy) sz
+            T m[R], wq[R];
+            if constexpr (FM) {
+                const T em = eplane ? T(1) : T(0);
+#pragma unroll
+                for (int r = 0; r < R; ++r) m[r] = om[r] * em, wq[r] = tq[HE][r][NQ - 1] * ortz;
+            }
+            sfor<D>([&](auto lc) {
+                constexpr int l = decltype(lc)::value;
+                constexpr int SE = (P + 4 - (D - 1) + l) & 3;  // slot of U_l(e)
+                T val[R];
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    if constexpr (l == D - 1) val[r] = ev[r];
+                    else val[r] = u[l][SE][r];
+                }
+                if constexpr (FM) {
+#pragma unroll
+                    for (int r = 0; r < R; ++r) {
+                        chk[l] += ovalid[r] ? val[r] : T(0);
+                        const T dv = (val[r] - fb[r] * p.ct[l]) * m[r];
+                        ma[l] = max_abs(ma[l], dv);
+                        mr[l].add(dv, wq[r]);
+                    }
+                } else {
+                    if (eplane) {
+#pragma unroll
+                        for (int r = 0; r < R; ++r) {
+                            if (!ovalid[r]) continue;
+                            chk[l] += val[r];
+                            accumulate_error_dev(val[r], fb[r] * p.ct[l], ma[l], mr[l]);
+                        }
+                    } else {
+#pragma unroll
+                        for (int r = 0; r < R; ++r)
+                            if (ovalid[r]) chk[l] += val[r];
+                    }
+                }
+            });
+        }
+        load_row(Ic<(P + 4 - (D - 1) + 1) & 1>{}, e + 1);
+    };
+
+    auto step = [&](auto phase, const int i) {
+        if (i < flo || i > fhi) plane(phase, std::true_type{}, i);  // seam / wrap / ends
+        else plane(phase, std::false_type{}, i);
+    };
+
+    // i = i0 .. ie + D - 1, unrolled by 4 so every slot index is a constant
+    for (int i = i0;;) {
+        step(Ph<0>{}, i);
+        if (++i > ie + D - 1) break;
+        step(Ph<1>{}, i);
+        if (++i > ie + D - 1) break;
+        step(Ph<2>{}, i);
+        if (++i > ie + D - 1) break;
+        step(Ph<3>{}, i);
+        if (++i > ie + D - 1) break;
+    }
+    sfor<D>([&](auto lc) {
+        constexpr int l = decltype(lc)::value;
+        T rel;
+        if constexpr (FM) rel = mr[l].value(p.ict[l]);
+        else rel = mr[l].value();
+        if constexpr (l > 0) __syncthreads();
+        commit_errors<T, NW>(ma[l], rel, chk[l], p.err[l]);
+    });
+}
+
+// load-pipeline variant (DEEP bits, see the top of the file): WAVE3D_TBN_DEEP, default kTbnDeep;
+// fp64 --math fma sweeps have all four, the others the default only
+constexpr int kTbnDeep = 0;
+int tbn_deep() {
+    static const int d = [] {
+        const char* e = std::getenv("WAVE3D_TBN_DEEP");
+        return e && *e ? std::atoi(e) & 3 : kTbnDeep;
+    }();
+    return d;
+}
+
+template <class T, int D, bool F>
+static void (*tbn_kernel(int rows, int waves, bool fm, int deep))(const TbnParams<T>) {
+    if (rows != 2 || waves != 8) return nullptr;
+    if (!fm) return deep == kTbnDeep ? k_tbn<T, D, F, 2, 8, false, kTbnDeep> : nullptr;
+    if constexpr (std::is_same_v<T, double>) {
+        switch (deep) {
+            case 0: return k_tbn<T, D, F, 2, 8, true, 0>;
+            case 1: return k_tbn<T, D, F, 2, 8, true, 1>;
+            case 2: return k_tbn<T, D, F, 2, 8, true, 2>;
+            case 3: return k_tbn<T, D, F, 2, 8, true, 3>;
+            default: return nullptr;
+        }
+    }
+    return deep == kTbnDeep ? k_tbn<T, D, F, 2, 8, true, kTbnDeep> : nullptr;
+}
+
+template <class T, bool F>
+static void (*tbn_kernel_d(int depth, int rows, int waves, bool fm, int deep))(const TbnParams<T>) {
+    if (depth == 4) return tbn_kernel<T, 4, F>(rows, waves, fm, deep);
+    if constexpr (std::is_same_v<T, double>)  // depth 3: fp64 (the cross-check of k_tb3, A/B)
+        if (depth == 3) return tbn_kernel<T, 3, F>(rows, waves, fm, deep);
+    return nullptr;
+}
+
+}  // namespace
+
+bool tbn_supported(int depth, int rows, int waves, bool fm) {
+    return tbn_kernel_d<double, false>(depth, rows, waves, fm, kTbnDeep) != nullptr;
+}
+
+template <class T>
+void launch_tbn(int depth, int rows, int waves, bool fm, bool first, const T* A, const T* B, T* O0, T* O1,
+                const GridView& gv, const Box* boxes, int nbox, const Box& cdom, int ei0, int ei1,
+                const Wrap& wrap0, const Wrap& wrap1, const TbnSeam<T>& seam, const T* txy, const T* tz,
+                const T* txr, const T* rtz, const StepCoefs* c, u64* const* err, int chunk, hipStream_t s) {
+    W3D_REQUIRE(depth >= 3 && depth <= kTbnMaxDepth, "tbn: depth 3..4");
+    W3D_REQUIRE(!fm || (txr && rtz), "tbn --math fma needs the reciprocal analytic tables");
+    W3D_REQUIRE(gv.G >= depth, "deep temporal blocking needs ghost depth >= layers per sweep");
+    W3D_REQUIRE(nbox >= 1 && nbox <= kMaxBoxes, "bad box count");
+    W3D_REQUIRE(gv.si * i64(sizeof(T)) < (i64(1) << 31), "tbn: plane larger than 2 GiB");
+    const int deep = tbn_deep();
+    auto kern = first ? tbn_kernel_d<T, true>(depth, rows, waves, fm, deep)
+                      : tbn_kernel_d<T, false>(depth, rows, waves, fm, deep);
+    W3D_REQUIRE(kern, "tbn: no instantiation of this depth x tile x dtype x math x WAVE3D_TBN_DEEP");
+    TbnParams<T> p{};
+    p.pbytes = unsigned(gv.si * i64(sizeof(T)));
+    p.pbias = gv.G + 1;  // plane indices reach ib - depth >= 1 - G and the wrap targets
+    p.order = tile_order();
+    auto biased = [&](const T* base) {
+        return reinterpret_cast<char*>(reinterpret_cast<uintptr_t>(base - gv.poff) - uintptr_t(p.pbias) * p.pbytes);
+    };
+    p.A = biased(A), p.B = biased(B), p.O[0] = biased(O0), p.O[1] = biased(O1);
+    p.sj = gv.sj;
+    p.poff = gv.poff;
+    p.jmin = 1 - gv.G, p.jmax = gv.jmax(), p.kmin = 1 - gv.G, p.kmax = gv.kmax();
+    p.cj0 = cdom.j0, p.cj1 = cdom.j1, p.ck0 = cdom.k0, p.ck1 = cdom.k1;
+    p.ei0 = ei0, p.ei1 = ei1;
+    wrap_ranges(wrap0, p.w_lo[0], p.w_hi[0], p.w_sh[0]);
+    wrap_ranges(wrap1, p.w_lo[1], p.w_hi[1], p.w_sh[1]);
+    p.an_i = seam.nP[0] ? seam.next_i : INT_MIN / 2;
+    p.ap_i = seam.pP[0] ? seam.prev_i : INT_MIN / 2;
+    for (int l = 0; l + 1 < depth; ++l) {
+        W3D_REQUIRE((!seam.nP[0] || seam.nP[l]) && (!seam.pP[0] || seam.pP[l]), "tbn: seam partner plane missing");
+        p.nP[l] = seam.nP[l], p.pP[l] = seam.pP[l];
+    }
+    p.txy = txy, p.tpj = gv.Y + 2, p.tz = tz;
+    p.txr = txr, p.rtz = rtz;
+    p.hx2 = T(c[0].hx2), p.hy2 = T(c[0].hy2), p.hz2 = T(c[0].hz2);
+    p.yx2 = T(1) / T(c[0].hx2), p.yy2 = T(1) / T(c[0].hy2), p.yz2 = T(1) / T(c[0].hz2);
+    for (int l = 0; l < depth; ++l) {
+        p.coef[l] = T(c[l].coef), p.ct[l] = T(c[l].ct), p.ict[l] = T(1 / std::fabs(c[l].ct));
+        p.err[l] = err[l];
+        W3D_REQUIRE(!fm || l == 0 || c[l].coef == c[1].coef, "tbn --math fma: the later layers share one coefficient");
+    }
+    W3D_REQUIRE(!fm || first || c[0].coef == c[1].coef, "tbn --math fma: one coefficient after the first sweep");
+    auto fcoefs = [](const StepCoefs& q, T out[3]) {
+        out[0] = T(q.coef / q.hx2), out[1] = T(q.coef / q.hy2), out[2] = T(q.coef / q.hz2);
+    };
+    fcoefs(c[0], p.fc[0]), fcoefs(c[1], p.fc[1]);
+    const int TJ = waves * rows;
+    int live = 0;
+    for (int q = 0; q < nbox; ++q) live += !boxes[q].empty();
+    const int extra = 2 * (depth - 1);  // prologue + epilogue planes of a work item
+    int multi_chunk = 0;
+    if (chunk <= 0 && live > 1) {
+        int bt[kMaxBoxes], bp[kMaxBoxes], m = 0;
+        for (int q = 0; q < nbox; ++q) {
+            const Box& bx = boxes[q];
+            if (bx.empty()) continue;
+            bt[m] = ((bx.k1 - 1) / kTK - (bx.k0 - 1) / kTK + 1) * cdiv(bx.j1 - bx.j0 + 1, TJ);
+            bp[m++] = bx.i1 - bx.i0 + 1;
+        }
+        multi_chunk = rounds_chunk_boxes(bt, bp, m, extra, resident_slots(reinterpret_cast<const void*>(kern), waves * 64));
+    }
+    int nb = 0, total = 0;
+    for (int q = 0; q < nbox; ++q) {
+        const Box& bx = boxes[q];
+        if (bx.empty()) continue;
+        W3D_REQUIRE(bx.i0 >= 1 && bx.i1 <= gv.X && bx.j0 >= 1 && bx.j1 <= gv.Y && bx.k0 >= 1 && bx.k1 <= gv.Z,
+                    "sweep box outside the owned region");
+        BoxLaunch& Lb = p.box[nb];
+        Lb.i0 = bx.i0, Lb.i1 = bx.i1, Lb.j0 = bx.j0, Lb.j1 = bx.j1, Lb.k0 = bx.k0, Lb.k1 = bx.k1;
+        const int t0 = (bx.k0 - 1) / kTK, t1 = (bx.k1 - 1) / kTK;
+        Lb.kbase = 1 + t0 * kTK;
+        Lb.tiles_k = t1 - t0 + 1;
+        Lb.tiles_j = cdiv(bx.j1 - bx.j0 + 1, TJ);
+        const int planes = bx.i1 - bx.i0 + 1;
+        const int want = chunk > 0 ? std::min(chunk, planes)
+                         : live == 1 ? rounds_chunk(planes, Lb.tiles_k * Lb.tiles_j, extra,
+                                                    resident_slots(reinterpret_cast<const void*>(kern), waves * 64))
+                                     : std::min(multi_chunk, planes);
+        Lb.chunk = cdiv(planes, cdiv(planes, want));
+        Lb.block_begin = total;
+        total += Lb.tiles_k * Lb.tiles_j * cdiv(planes, Lb.chunk);
+        ++nb;
+    }
+    p.nbox = nb;
+    if (nb == 0) return;
+    hipLaunchKernelGGL(kern, dim3(total), dim3(waves * 64), 0, s, p);
+    HIP_OK(hipGetLastError());
+}
+
+#define W3D_TBN_INST(T)                                                                                          \
+    template void launch_tbn<T>(int, int, int, bool, bool, const T*, const T*, T*, T*, const GridView&,         \
+                                const Box*, int, const Box&, int, int, const Wrap&, const Wrap&,                \
+                                const TbnSeam<T>&, const T*, const T*, const T*, const T*, const StepCoefs*,   \
+                                u64* const*, int, hipStream_t);
+W3D_TBN_INST(double)
+W3D_TBN_INST(float)
+
+}  // namespace wave3d

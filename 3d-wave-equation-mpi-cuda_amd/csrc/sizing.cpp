@@ -7,9 +7,9 @@
 
 namespace wave3d {
 
-// "tb2[r<R>][w<W>][k<NWK>][o<OCC>]" / "tb3[r<R>w<W>]"
+// "tb2[r<R>][w<W>][k<NWK>][o<OCC>]" / "tb3[r<R>w<W>]" / "tb4[r<R>w<W>]"
 static void parse_tb(const std::string& name, int& rows, int& waves, int& occ, int& kwaves) {
-    if (name.rfind("tb3", 0) != 0) rows = 2, waves = 4;
+    if (name.rfind("tb3", 0) != 0 && name.rfind("tb4", 0) != 0) rows = 2, waves = 4;
     occ = 0;
     kwaves = 1;
     std::string s = name.substr(3);
@@ -43,16 +43,19 @@ Layout plan_layout(const Config& c, int world) {
     // fp64 exact leapfrog: tb3 too since the scalar diet — 373-374k vs tb2r2w8 317k Mpts/s at
     // N=512, bitwise equal (profiles/tb3_salu_r3.txt); the fp64 increment form stays on tb2r2w4
     const bool auto_tb3 = auto_tb && (c.dtype == DType::F32 || c.fma || !c.delta);
-    const bool tb3 = auto_tb3 || c.kernel.rfind("tb3", 0) == 0;
-    l.tb = auto_tb || tb3 || c.kernel.rfind("tb2", 0) == 0;
-    l.depth = tb3 ? 3 : (l.tb ? 2 : 1);
-    if (tb3) l.rows = 2, l.waves = 8;  // measured best three-layer tile (profiles/)
+    const bool tbn3 = c.kernel.rfind("tbn3", 0) == 0;  // k_tbn at depth 3 (A/B of k_tb3)
+    const bool tb4 = c.kernel.rfind("tb4", 0) == 0;
+    const bool tb3 = !tb4 && (auto_tb3 || tbn3 || c.kernel.rfind("tb3", 0) == 0);
+    l.generic = tb4 || tbn3;
+    l.tb = auto_tb || tb3 || tb4 || c.kernel.rfind("tb2", 0) == 0;
+    l.depth = tb4 ? 4 : (tb3 ? 3 : (l.tb ? 2 : 1));
+    if (tb3 || tb4) l.rows = 2, l.waves = 8;  // measured best three-layer tile (profiles/)
     // 16-row tiles of 8 waves (tb2r2w8, 2 workgroups per CU): fp64 +2-3 % over r2w4 (128
     // VGPRs, 4 waves/SIMD), fp32 +3.5 % (N=512) / +5 % (N=2048) over tb2r4 (profiles/
     // ab_tiles_r2.txt, fp32_accuracy_r2.txt). The fp64 increment form needs a few more
     // registers: r2w8 drops to 3 waves/SIMD there, so it keeps the 8-row r2w4 tiles.
     if (auto_tb && !(c.delta && c.dtype == DType::F64)) l.waves = 8;
-    if (l.tb && !auto_tb) parse_tb(c.kernel, l.rows, l.waves, l.occ, l.kwaves);
+    if (l.tb && !auto_tb) parse_tb(tbn3 ? "tb3" + c.kernel.substr(4) : c.kernel, l.rows, l.waves, l.occ, l.kwaves);
     l.G = l.depth;      // ghost depth = layers per sweep
     // time levels: one stored layer per single step -> 3; a sweep stores two layers (tb2: u^m and
     // u^{m+1}; tb3: D and E, C never stored) and reads two -> 4 (hip_solver plan_slots)

@@ -12,7 +12,8 @@ namespace wave3d {
 // Kernel family and storage shape the HIP solver picks for a configuration.
 struct Layout {
     bool tb = false;          // temporal blocking
-    int depth = 1;            // layers per sweep: 1 (single step), 2 (tb2) or 3 (tb3)
+    int depth = 1;            // layers per sweep: 1 (single step), 2 (tb2), 3 (tb3) or 4 (tb4)
+    bool generic = false;     // deep sweeps through the depth-generic kernel (k_tbn; "tbn3")
     int rows = 2, waves = 4;  // TB tile shape
     int occ = 0;              // TB register cap (min waves per SIMD, 0 = compiler's choice)
     int kwaves = 1;           // TB waves side by side along k (tile width 64 * kwaves)

@@ -30,8 +30,8 @@ CONFIGS = {
     "gpu1024x4": dict(problem=WaveProblem(1024, timesteps=100), backend="hip", Np=4, dims=[2, 2, 1]),
     # N=1024^3 fp64 on 8 MI355X, 2x2x2 blocks (6-face deep halos, interior/shell overlap)
     "gpu1024x8": dict(problem=WaveProblem(1024, timesteps=100), backend="hip", Np=8, dims=[2, 2, 2]),
-    # N=2048^3 fp32 on 8 MI355X; the increment form (profiles/fp32_scheme_r3.txt: ~6x lower
-    # L-inf than fp32 leapfrog for ~6 % throughput)
+    # N=2048^3 fp32 on 8 MI355X; the increment form (profiles/fp32_scheme_r4.txt: 6.3x lower
+    # L-inf than fp32 leapfrog, and 3 % faster on the tb3 sweep)
     "gpu2048x8_fp32": dict(problem=WaveProblem(2048, timesteps=200, dtype="fp32", scheme="delta"), backend="hip",
                            Np=8, dims=None),
 }
@@ -41,8 +41,9 @@ def default_scheme(dtype: str) -> str:
     """Time-stepping form for a precision. fp64: the reference's leapfrog (bitwise parity with
     its error tables). fp32: the increment form u^n = u^{n-1} + d^n, d^n = d^{n-1} + a2 tau^2
     lap u^{n-1} — the same scheme in exact arithmetic, without leapfrog's 2u - u cancellation that
-    sets the fp32 error floor (mpi_new.cpp:338); measured 3.4x (N=512) / 6.3x (N=2048) lower
-    L-inf for 7.7 % / 6.4 % throughput (profiles/tb3_diet_r2.txt, fp32_scheme_r3.txt)."""
+    sets the fp32 error floor (mpi_new.cpp:338); measured 3.2x (N=512) / 6.3x (N=2048) lower
+    L-inf at +3 % throughput on the tb3 sweep (profiles/fp32_scheme_r4.txt; round 2, tb2:
+    profiles/fp32_accuracy_r2.txt)."""
     return "leapfrog" if dtype == "fp64" else "delta"
 
 

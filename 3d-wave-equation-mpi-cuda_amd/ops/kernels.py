@@ -204,6 +204,31 @@ def tb_sweep(A, B, C, D, boxes, *, first: bool, cdom, err_i, tx, ty, tz, coefs_c
        err_d.data_ptr(), int(chunk), _stream())
 
 
+def tbn_sweep(A, B, O0, O1, boxes, *, depth: int, first: bool, cdom, err_i, tx, ty, tz, coefs, errs,
+              rows: int = 2, waves: int = 8, chunk: int = 0, ghost: int | None = None, fma: bool = False) -> None:
+    """One deep sweep (k_tbn, ``depth`` layers u^m .. u^{m+depth-1}): the first depth-2 layers
+    errors only, O0 = u^{m+depth-2}, O1 = u^{m+depth-1}. ``coefs[l]`` = (hx2, hy2, hz2, coef, ct)
+    and ``errs[l]`` the error slot of layer m+l."""
+    ghost = depth if ghost is None else ghost
+    gv = _check_grid_g(ghost, A, B, O0, O1)
+    if ghost < depth:
+        raise ValueError("k_tbn needs ghost depth >= depth")
+    if isinstance(boxes[0], int):
+        boxes = [boxes]
+    bl = [_check_box_g(b, gv) for b in boxes]
+    if not _C().tbn_supported(int(depth), int(rows), int(waves), bool(fma)):
+        raise ValueError(f"unsupported depth={depth} tile rows={rows} waves={waves} fma={fma}")
+    if len(coefs) != depth or len(errs) != depth:
+        raise ValueError("one coefficient set and one error slot per layer")
+    for t in (tx, ty, tz):
+        if not t.is_cuda or t.dtype != A.dtype or t.numel() < max(gv[:3]):
+            raise ValueError("analytic tables must be device tensors covering the grid")
+    fn = getattr(_C(), "k_tbn_" + _sfx(A))
+    fn(int(depth), int(rows), int(waves), bool(fma), bool(first), A.data_ptr(), B.data_ptr(), O0.data_ptr(),
+       O1.data_ptr(), gv, bl, [int(v) for v in cdom], int(err_i[0]), int(err_i[1]), tx.data_ptr(), ty.data_ptr(),
+       tz.data_ptr(), [[float(c) for c in co] for co in coefs], [e.data_ptr() for e in errs], int(chunk), _stream())
+
+
 def tb3_sweep(A, B, D, E, boxes, *, first: bool, cdom, err_i, tx, ty, tz, coefs_c, coefs_d,
               coefs_e, err_c, err_d, err_e, rows: int = 2, waves: int = 8, chunk: int = 0,
               ghost: int = 3, fma: bool = False) -> None:

@@ -479,3 +479,75 @@ def test_fma_math_matches_oracle(C, kernel, scheme, dtype, ranks):
     assert g.max_abs == c.max_abs
     for a, b in zip(g.max_rel, c.max_rel):
         assert a == pytest.approx(b, rel=1e-9 if dtype == "fp64" else 1e-4)
+
+
+# ---- four-layer temporal blocking (k_tbn, depth 4) -------------------------------------------
+@pytest.mark.parametrize("K", [9, 10, 11, 12, 13])
+@pytest.mark.parametrize("math_", ["exact", "fma"])
+def test_tb4_single_rank_bitwise(C, K, math_):
+    """Four layers per sweep (two in registers, seam partners of two layers from the two-stage
+    seam pre-kernel, periodic self-wrap of depth 3 / 4) with three-, two-layer and single-step
+    tails: bitwise equal to the OpenMP oracle (shifted IC: the periodic seam is exercised)."""
+    import wave3d
+
+    p = wave3d.WaveProblem(40, Lx=1.3, Ly="pi", Lz=2.0, timesteps=K, ic="shifted", math=math_)
+    base = _solve(p, backend="cpu", threads=4)
+    r = _solve(p, kernel="tb4")
+    assert r.kernel == "tb4" and r.extra["math"] == math_
+    assert r.max_abs == base.max_abs
+    if math_ == "exact":
+        assert r.max_rel == base.max_rel
+    else:
+        for a, b in zip(r.max_rel, base.max_rel):
+            assert a == pytest.approx(b, rel=1e-9)
+
+
+@pytest.mark.parametrize("ranks,dims,overlap", [(2, None, True), (3, None, False), (4, None, True),
+                                                (8, [2, 2, 2], True), (8, [2, 2, 2], False),
+                                                (4, [1, 2, 2], False), (2, [1, 1, 2], True)])
+def test_tb4_multi_rank_bitwise(C, ranks, dims, overlap):
+    """Simulated ranks (loopback halos of depth 4 / 3, seam alias planes on x splits) with and
+    without the interior/shell overlap: bitwise equal to the OpenMP oracle."""
+    import wave3d
+
+    for K in (12, 14):
+        p = wave3d.WaveProblem(47, Lx=1.3, Ly="pi", Lz=2.0, timesteps=K, ic="shifted")
+        base = _solve(p, backend="cpu", threads=4)
+        r = _solve(p, ranks=ranks, dims=dims, overlap=overlap, kernel="tb4")
+        assert r.kernel == "tb4"
+        assert r.max_abs == base.max_abs and r.max_rel == base.max_rel
+
+
+def test_tb4_resume_fault_and_goldens(C, tmp_path):
+    """Checkpoint / resume across four-layer sweeps (resume re-plans the level ring), fault
+    detection, the N=32 golden table and the headline N=512 K=100 L-inf with --math fma."""
+    import wave3d
+    from wave3d.utils import GOLDEN_N32_K20, GOLDEN_SPOTS
+
+    p = wave3d.WaveProblem(40, timesteps=17, ic="shifted")
+    full = _solve(p, kernel="tb4", ranks=2)
+    _solve(p, kernel="tb4", ranks=2, checkpoint_every=6, checkpoint_dir=str(tmp_path))
+    res = _solve(p, kernel="tb4", ranks=2, resume=str(tmp_path))
+    assert res.extra["resumed_from"] == 12
+    assert res.max_abs == full.max_abs and res.max_rel == full.max_rel
+    bad = _solve(p, kernel="tb4", ranks=2, fault="nan:1:5", check_every=1)
+    assert bad.aborted
+    assert _fmt(_solve(wave3d.WaveProblem(32, timesteps=20), kernel="tb4")) == GOLDEN_N32_K20
+    got = _fmt(_solve(wave3d.WaveProblem(512, timesteps=100, math="fma"), kernel="tb4"))
+    for layer, (a, _) in GOLDEN_SPOTS[(512, 100, "ref")].items():
+        assert got[layer][0] == a
+
+
+@pytest.mark.parametrize("dims", ["2,2,2", "1,2,2"])
+@pytest.mark.parametrize("K", [40, 42])
+def test_tb4_overlap_concurrent_interior_bitwise(C, dims, K):
+    """N=160 with a non-empty tile-aligned interior on 3-D block decompositions: the overlapped
+    four-layer sweeps are bitwise equal to the OpenMP oracle."""
+    import wave3d
+
+    p = wave3d.WaveProblem(160, Lx=1.3, Ly="pi", Lz=2.0, timesteps=K, ic="shifted")
+    d = [int(x) for x in dims.split(",")]
+    r = _solve(p, ranks=d[0] * d[1] * d[2], dims=d, overlap=True, kernel="tb4")
+    assert r.extra["overlap"] is True and r.extra["overlap_interior"] > 0
+    ref = _solve(p, backend="cpu", threads=8)
+    assert r.max_abs == ref.max_abs and r.max_rel == ref.max_rel

@@ -241,3 +241,145 @@ def test_tb3_fma_sweep_close_to_reference(C, dtype, first, rows, waves, case):
         s = _sl(b, G)
         torch.testing.assert_close(gD[s].double(), Df[s], **tol)
         torch.testing.assert_close(gE[s].double(), Ef[s], **tol)
+    if len(boxes) == 1:  # the fused error keys of all three layers
+        s = _sl(boxes[0], G)
+        for err, vals, q in ((errs[0], Cf[s], 0), (errs[1], Df[s], 1), (errs[2], Ef[s], 2)):
+            _check_err_fma(err, vals, boxes[0], ei, tx, ty, tz, CT[q], dtype)
+
+
+def _check_err_fma(err, vals, box, ei, tx, ty, tz, ct, dtype):
+    """--math fma error keys vs the fp64 oracle: |u - f| to 1e-12 relative, |u - f|/|f| (taken as
+    |d| * 1/|sx sy| * 1/|sz| / |ct| in the sweep) to 1e-9; fp32 to its rounding."""
+    from wave3d.ops import kernels, reference
+
+    i0, i1, j0, j1, k0, k1 = box
+    f = reference.analytic(tx[ei[0]:ei[1] + 1].double(), ty[j0:j1 + 1].double(), tz[k0:k1 + 1].double(),
+                           float(torch.tensor(ct, dtype=dtype).item()))
+    ea, er = reference.max_errors(vals[ei[0] - i0:ei[1] - i0 + 1].double(), f)
+    (ga, gr, bad), = kernels.decode_err(err)
+    ra, rr = (1e-12, 1e-9) if dtype == torch.float64 else (1e-5, 1e-4)
+    assert math.isclose(ga, ea, rel_tol=ra) and math.isclose(gr, er, rel_tol=rr)
+    assert not bad
+
+
+TBN_CASES = [
+    # (X, Y, Z), boxes, cdom, chunk — as CASES, with a box that starts past the first plane and
+    # chunks short enough that every work item runs its prologue / epilogue planes
+    ((11, 40, 131), [(2, 10, 3, 37, 60, 130)], (1, 11, 1, 40, 1, 130), 3),
+    ((11, 40, 131), [(1, 11, 1, 40, 1, 130)], (1, 11, 1, 40, 1, 130), 0),
+    ((13, 21, 70), [(1, 2, 1, 21, 1, 69), (3, 13, 5, 9, 2, 66)], (1, 13, 1, 21, 1, 69), 5),
+    ((9, 9, 11), [(1, 9, 2, 8, 2, 10)], (1, 9, 2, 8, 2, 10), 0),
+]
+
+
+@pytest.mark.parametrize("first", [False, True])
+@pytest.mark.parametrize("fma", [False, True])
+@pytest.mark.parametrize("case", range(len(TBN_CASES)))
+def test_tbn_depth3_bitwise_equal_to_tb3(C, first, fma, case):
+    """The generic deep sweep at depth 3 is the three-layer sweep: k_tbn<3> and k_tb3 on the
+    same fields give bitwise identical D, E and error keys (fp64, exact and --math fma)."""
+    from wave3d.ops import kernels
+
+    (X, Y, Z), boxes, cdom, chunk = TBN_CASES[case]
+    G, dtype = 4, torch.float64
+    shape = (X + 2 * G, Y + 2 * G, Z + 2 * G)
+    A, B = _rand(shape, dtype, 14).to(DEV), _rand(shape, dtype, 15).to(DEV)
+    tx, ty, tz = (t.to(DEV) for t in _tables(max(shape), dtype, 16))
+    ei = (min(b[0] for b in boxes), max(b[1] for b in boxes))
+    coefs = (COEFS[0] if first or not fma else COEFS[1], COEFS[1], COEFS[2] if not fma else COEFS[1])
+    co = [(*COEF.values(), coefs[q], CT[q]) for q in range(3)]
+    outs = []
+    for tbn in (False, True):
+        dD, dE = (torch.full(shape, v, dtype=dtype, device=DEV) for v in (-7.0, -9.0))
+        errs = [kernels.new_err(1) for _ in range(3)]
+        kw = dict(first=first, cdom=cdom, err_i=ei, tx=tx, ty=ty, tz=tz, rows=2, waves=8, chunk=chunk,
+                  ghost=G, fma=fma)
+        if tbn:
+            kernels.tbn_sweep(A, B, dD, dE, boxes, depth=3, coefs=co, errs=errs, **kw)
+        else:
+            kernels.tb3_sweep(A, B, dD, dE, boxes, coefs_c=co[0], coefs_d=co[1], coefs_e=co[2], err_c=errs[0],
+                              err_d=errs[1], err_e=errs[2], **kw)
+        torch.cuda.synchronize()
+        outs.append((dD.cpu(), dE.cpu(), [e.cpu() for e in errs]))
+    (d0, e0, k0), (d1, e1, k1) = outs
+    assert torch.equal(d0, d1) and torch.equal(e0, e1)
+    for a, b in zip(k0, k1):
+        assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
+@pytest.mark.parametrize("first", [False, True])
+@pytest.mark.parametrize("case", range(len(TBN_CASES)))
+def test_tbn_depth4_sweep_matches_reference(C, dtype, first, case):
+    """Four layers per sweep (k_tbn<4>, exact arithmetic): the stored layers u^{m+2}, u^{m+3} and
+    the error keys of all four layers against the chained plain-PyTorch oracle — bitwise in fp64;
+    nodes outside the boxes untouched."""
+    from wave3d.ops import kernels, reference
+
+    (X, Y, Z), boxes, cdom, chunk = TBN_CASES[case]
+    G = 4
+    shape = (X + 2 * G, Y + 2 * G, Z + 2 * G)
+    A, B = _rand(shape, dtype, 24), _rand(shape, dtype, 25)
+    tx, ty, tz = _tables(max(shape), dtype, 26)
+    c4 = (3.1e-4, 2.9e-4, 2.7e-4, 2.6e-4)
+    ct4 = (-0.83, 0.47, 0.21, -0.66)
+    dO0, dO1 = (torch.full(shape, v, dtype=dtype, device=DEV) for v in (-7.0, -9.0))
+    errs = [kernels.new_err(1) for _ in range(4)]
+    ei = (min(b[0] for b in boxes), max(b[1] for b in boxes))
+    co = [(*COEF.values(), c4[q], ct4[q]) for q in range(4)]
+    kernels.tbn_sweep(A.to(DEV), B.to(DEV), dO0, dO1, boxes, depth=4, first=first, cdom=cdom, err_i=ei,
+                      tx=tx.to(DEV), ty=ty.to(DEV), tz=tz.to(DEV), coefs=co, errs=errs, chunk=chunk)
+    torch.cuda.synchronize()
+    cast = lambda v: torch.tensor(v, dtype=dtype).item()  # noqa: E731
+    h = {k: cast(v) for k, v in COEF.items()}
+    L = reference.chained_layers(A, B, 4, first=first, mask=_mask(shape, G, cdom), coefs=[cast(c) for c in c4], **h)
+    g0, g1 = dO0.cpu(), dO1.cpu()
+    touched = torch.zeros(shape, dtype=torch.bool)
+    for b in boxes:
+        s = _sl(b, G)
+        _check(g0[s], L[2][s], dtype)
+        _check(g1[s], L[3][s], dtype)
+        touched[s] = True
+    assert bool((g0[~touched] == -7.0).all()) and bool((g1[~touched] == -9.0).all())
+    if len(boxes) == 1:
+        s = _sl(boxes[0], G)
+        for q in range(4):
+            _check_err(errs[q], L[q][s], boxes[0], ei, tx, ty, tz, ct4[q], dtype)
+
+
+@pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
+@pytest.mark.parametrize("first", [False, True])
+@pytest.mark.parametrize("case", range(len(TBN_CASES)))
+def test_tbn_depth4_fma_close_to_reference(C, dtype, first, case):
+    """The --math fma four-layer sweep (the fp64 bench kernel) within a few ulps of the fp64
+    chained oracle, error keys included."""
+    from wave3d.ops import kernels, reference
+
+    (X, Y, Z), boxes, cdom, chunk = TBN_CASES[case]
+    G = 4
+    shape = (X + 2 * G, Y + 2 * G, Z + 2 * G)
+    A, B = _rand(shape, dtype, 34), _rand(shape, dtype, 35)
+    tx, ty, tz = _tables(max(shape), dtype, 36)
+    c = 2.9e-4
+    c4 = (3.1e-4 if first else c, c, c, c)
+    ct4 = (-0.83, 0.47, 0.21, -0.66)
+    dO0, dO1 = (torch.full(shape, v, dtype=dtype, device=DEV) for v in (-7.0, -9.0))
+    errs = [kernels.new_err(1) for _ in range(4)]
+    ei = (min(b[0] for b in boxes), max(b[1] for b in boxes))
+    co = [(*COEF.values(), c4[q], ct4[q]) for q in range(4)]
+    kernels.tbn_sweep(A.to(DEV), B.to(DEV), dO0, dO1, boxes, depth=4, first=first, cdom=cdom, err_i=ei,
+                      tx=tx.to(DEV), ty=ty.to(DEV), tz=tz.to(DEV), coefs=co, errs=errs, chunk=chunk, fma=True)
+    torch.cuda.synchronize()
+    h = {k: float(v) for k, v in COEF.items()}
+    L = reference.chained_layers(A.double(), B.double(), 4, first=first, mask=_mask(shape, G, cdom),
+                                 coefs=list(c4), **h)
+    tol = dict(rtol=1e-12, atol=1e-12) if dtype == torch.float64 else dict(rtol=4e-5, atol=4e-5)
+    g0, g1 = dO0.cpu(), dO1.cpu()
+    for b in boxes:
+        s = _sl(b, G)
+        torch.testing.assert_close(g0[s].double(), L[2][s], **tol)
+        torch.testing.assert_close(g1[s].double(), L[3][s], **tol)
+    if len(boxes) == 1:
+        s = _sl(boxes[0], G)
+        for q in range(4):
+            _check_err_fma(errs[q], L[q][s], boxes[0], ei, tx, ty, tz, ct4[q], dtype)

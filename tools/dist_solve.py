@@ -39,11 +39,17 @@ def main():
         torch.cuda.set_device(dev)
         args += ["--device", str(dev)]
     wdist.init_from_env("nccl" if a.transport == "rccl" else "gloo", force=True)
-    tr = wdist.make_transport(a.transport, a.backend)
+    mode = "auto"
+    for q, x in enumerate(args):
+        if x == "--no-overlap":
+            mode = "off"
+        elif x == "--overlap":
+            mode = args[q + 1] if q + 1 < len(args) and args[q + 1] in ("on", "off", "auto") else "on"
+    tr = wdist.make_transport(a.transport, a.backend, overlap=mode)
     r = C.run(args, a.backend, tr, False, rank == 0)
     if rank == 0:
         keep = ("N", "timesteps", "nprocs", "dims", "transport", "kernel", "max_abs", "max_rel",
-                "total_ms", "loop_ms", "exchange_ms", "comm_ms", "overlap", "comm_size",
+                "total_ms", "loop_ms", "exchange_ms", "comm_ms", "overlap", "comm_size", "rccl_max_ctas",
                 "solve_ms", "mpts_per_s_best",
                 "aborted", "abort_layer", "resumed_from")
         print("RESULT " + json.dumps({k: r[k] for k in keep}), flush=True)
