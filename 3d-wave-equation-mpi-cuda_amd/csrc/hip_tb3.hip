@@ -37,6 +37,15 @@
 #ifndef W3D_TB3_ABL
 #define W3D_TB3_ABL 0
 #endif
+// LDS row pitch padding (doubles/floats added to the even tile widths): 1 makes the pitches odd,
+// so a ring column (lanes at one k, consecutive rows) hits 32 distinct ds_read_b64 bank pairs
+#ifndef W3D_TB3_PAD
+#define W3D_TB3_PAD 0
+#endif
+// B slots: 2 = B(i+1) prefetched at iteration i, 4 = B(i+2) (two planes of load latency)
+#ifndef W3D_TB3_NB
+#define W3D_TB3_NB 2
+#endif
 
 namespace wave3d {
 namespace {
@@ -98,9 +107,9 @@ template <class T, bool FIRST, int R, int NW, bool DELTA = false, bool FM = fals
           int WPE = (R == 1 || (DELTA && sizeof(T) == 4) ? 4 : 1)>
 __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WPE, 8))) k_tb3(const Tb3Params<T> p) {
     constexpr int TJ = NW * R;
-    constexpr int AH = TJ + 6, AW = kTK + 6;  // A tile origin (jt-3, kb-3)
-    constexpr int CH = TJ + 4, CW = kTK + 4;  // C tile origin (jt-2, kb-2)
-    constexpr int DH = TJ + 2, DW = kTK + 2;  // D tile origin (jt-1, kb-1)
+    constexpr int AH = TJ + 6, AW = kTK + 6 + W3D_TB3_PAD;  // A tile origin (jt-3, kb-3)
+    constexpr int CH = TJ + 4, CW = kTK + 4 + W3D_TB3_PAD;  // C tile origin (jt-2, kb-2)
+    constexpr int DH = TJ + 2, DW = kTK + 2 + W3D_TB3_PAD;  // D tile origin (jt-1, kb-1)
     constexpr int N1 = 2 * kTK + 2 * (TJ + 2);        // 1-ring positions
     constexpr int N2 = 2 * (kTK + 2) + 2 * (TJ + 4);  // 2-ring positions
     constexpr int N3 = 2 * (kTK + 4) + 2 * (TJ + 4);  // 3-ring positions (A only, no corners)
@@ -242,15 +251,16 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WP
     //   C(x), ring C(x): (x - ib + 2) & 3  -> C(i) = P, C(i-1) = P+3, C(i-2) = P+2
     //   D(x): (x - ib + 3) & 3             -> D(i-1) = P, D(i-2) = P+3, D(i-3) = P+2
     //   B(x), ring B(x), LDS buffers: (x - ib + 2) & 1
-    T a[4][R], c[4][R], d[4][R], bb[2][R];
-    T ra[RP][4], rb[RP][2], rc[RP][4];
+    constexpr int NB = W3D_TB3_NB, BD = NB / 2;  // B slots, B prefetch distance (planes)
+    T a[4][R], c[4][R], d[4][R], bb[NB][R];
+    T ra[RP][4], rb[RP][NB], rc[RP][4];
     // increment form: d^m of own planes i (H0) / i-1 (H1) and of the ring, d^{m+1} of own
     // planes i-1 (H0) / i-2 (H1)
     constexpr int ND = DELTA ? 2 : 1;
     T dm[ND][R], dm1[ND][R], rdm[RP][ND];
     {
         const auto r0 = prl(p.A, ib - 3, pbytes), rA1 = prl(p.A, ib - 2, pbytes), rA2 = prl(p.A, ib - 1, pbytes);
-        const auto rB = prl(p.B, ib - 2, pbytes);
+        const auto rB = prl(p.B, ib - 2, pbytes), rBn = prl(p.B, ib - 1, NB == 4 ? pbytes : 0u);
 #pragma unroll
         for (int r = 0; r < R; ++r) {
             a[0][r] = bld<T>(r0, oa[r]);
@@ -258,7 +268,8 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WP
             a[2][r] = bld<T>(rA2, oa[r]);
             a[3][r] = T(0);
             bb[0][r] = bld<T>(rB, ob[r]);
-            bb[1][r] = T(0);
+#pragma unroll
+            for (int t = 1; t < NB; ++t) bb[t][r] = t == 1 && NB == 4 ? bld<T>(rBn, ob[r]) : T(0);
 #pragma unroll
             for (int s = 0; s < 4; ++s) c[s][r] = d[s][r] = T(0);
         }
@@ -269,7 +280,8 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WP
             ra[s][2] = bld<T>(rA2, ra_off[s]);
             ra[s][3] = T(0);
             rb[s][0] = bld<T>(rB, rb_off[s]);
-            rb[s][1] = T(0);
+#pragma unroll
+            for (int t = 1; t < NB; ++t) rb[s][t] = t == 1 && NB == 4 ? bld<T>(rBn, rb_off[s]) : T(0);
 #pragma unroll
             for (int t = 0; t < 4; ++t) rc[s][t] = T(0);
         }
@@ -399,23 +411,24 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WP
         constexpr bool FAST = !ALIAS;
         constexpr int S0 = P & 3, S1 = (P + 1) & 3, S2 = (P + 2) & 3, S3 = (P + 3) & 3;
         constexpr int H0 = P & 1, H1 = (P + 1) & 1;
+        constexpr int BC = P & (NB - 1), BP = (P + BD) & (NB - 1);  // B(i), B(i+BD) slots
 
-        // ---- prefetch A(i+2), B(i+1) (own and ring; 0-record descriptors when done) --------
+        // ---- prefetch A(i+2), B(i+BD) (own and ring; 0-record descriptors when done) -------
         {
-            const bool more = FAST || i <= ie + 1;
+            const bool more = FAST || i <= ie + 1, moreB = FAST || i + BD <= ie + 2;
             const unsigned nb = more ? pbytes : 0u;
-            const int d2 = more ? 2 : 0, d1 = more ? 1 : 0;
+            const int d2 = more ? 2 : 0, d1 = moreB ? BD : 0;
             const auto rA2 = prl(p.A, i + d2, nb);
-            const auto rB1 = prl(p.B, i + d1, nb);
+            const auto rB1 = prl(p.B, i + d1, moreB ? pbytes : 0u);
 #pragma unroll
             for (int r = 0; r < R; ++r) {
                 a[S3][r] = bld<T>(rA2, oa[r]);
-                bb[H1][r] = bld<T>(rB1, ob[r]);
+                bb[BP][r] = bld<T>(rB1, ob[r]);
             }
 #pragma unroll
             for (int s = 0; s < RP; ++s) {
                 ra[s][S3] = bld<T>(rA2, ra_off[s]);
-                rb[s][H1] = bld<T>(rB1, rb_off[s]);
+                rb[s][BP] = bld<T>(rB1, rb_off[s]);
             }
         }
         // ---- stage A(i) --------------------------------------------------------------------
@@ -472,11 +485,11 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WP
             const int y = 3 + w * R + r, x = 3 + lane;
             const T lap = lapA(H0, y, x, a[S1][r], xpA[r], xnA[r]);
             if constexpr (DELTA) {
-                const T dv = FIRST ? scaled(0, lap) : incr(0, bb[H0][r], lap);
+                const T dv = FIRST ? scaled(0, lap) : incr(0, bb[BC][r], lap);
                 dm[H0][r] = ocd[r] ? dv : T(0);
                 c[S0][r] = ocd[r] ? a[S1][r] + dv : T(0);  // FIRST: = taylor_first
             } else {
-                c[S0][r] = ocd[r] ? cval(a[S1][r], bb[H0][r], lap) : T(0);
+                c[S0][r] = ocd[r] ? cval(a[S1][r], bb[BC][r], lap) : T(0);
             }
             ldsC[H0][y - 1][x - 1] = c[S0][r];
         }
@@ -486,11 +499,11 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WP
                 const T lap = lapA(H0, ry[s], rx[s], ra[s][S1], rxp[s], rxn[s]);
                 T cv;
                 if constexpr (DELTA) {
-                    const T dv = FIRST ? scaled(0, lap) : incr(0, rb[s][H0], lap);
+                    const T dv = FIRST ? scaled(0, lap) : incr(0, rb[s][BC], lap);
                     rdm[s][H0] = rcd[s] ? dv : T(0);
                     cv = rcd[s] ? ra[s][S1] + dv : T(0);
                 } else {
-                    cv = rcd[s] ? cval(ra[s][S1], rb[s][H0], lap) : T(0);
+                    cv = rcd[s] ? cval(ra[s][S1], rb[s][BC], lap) : T(0);
                 }
                 rc[s][S0] = cv;
                 ldsC[H0][ry[s] - 1][rx[s] - 1] = cv;

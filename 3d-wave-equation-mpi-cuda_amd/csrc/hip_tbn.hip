@@ -17,10 +17,13 @@
 // indexed by plane number mod 4 / mod 2 with the i loop unrolled by 4 (no copies of in-flight
 // loads): U_l(x) lives in slot (x + l - i0) & 3, i.e. the phase of the iteration that made it.
 //
-// Ring ownership (as k_tb3): every ring node belongs to ONE thread — rings 1..D-1 whole, ring D
-// (A only) without its corners, which no in-plane 5-point stencil of layer 0 reads — RP
-// positions per thread. A slot whose first possible ring is r only carries the history of the
-// layers evaluated on ring r (compile-time), so the far rings cost registers for A and B only.
+// Ring ownership (as k_tb3): every ring node belongs to ONE thread, RP positions per thread, in
+// the order rings 1..D-2 whole, ring D-1 without its corners (no later layer reads layer 0
+// there), then the staging-only positions: the four ring-(D-1) corners (A there is read by layer
+// 0 on the adjacent ring-(D-1) nodes) and ring D without corners. With 16-row tiles the compute
+// positions of D = 4 are exactly 512 (one per thread of 8 waves), so the second slot only
+// stages A. A slot whose first possible ring is r only carries the history of the layers
+// evaluated on ring r (compile-time), so the far rings cost registers for A and B only.
 //
 // Load pipeline depth (DEEP bits): bit 0 — A is prefetched three planes ahead instead of two: A(i-1)
 // is read from the LDS tile staged last iteration (still intact until the next barrier), so its
@@ -94,12 +97,18 @@ template <int D, int TJ>
 struct TbnGeom {
     // staged layer s: 0 = A (ring D), s >= 1 = U_{s-1} (ring D - s); frame origin (s, s)
     static constexpr int H(int s) { return TJ + 2 * (D - s); }
-    static constexpr int W(int s) { return kTK + 2 * (D - s); }
+    // row pitch: the staged width rounded up to odd, so the lanes of a ring column (one k,
+    // consecutive rows) hit 32 distinct ds_read_b64 bank pairs (an even pitch of 72 doubles put
+    // 8 rows on one pair: 4.6x the bank-conflict cycles of k_tb3 in the first tb4 PMC)
+    static constexpr int W(int s) { return (kTK + 2 * (D - s)) | 1; }
     static constexpr int size(int s) { return H(s) * W(s); }
     static constexpr int off(int s) { return s == 0 ? 0 : off(s - 1) + 2 * size(s - 1); }
     static constexpr int total = off(D);
-    // ring r positions: rings 1..D-1 whole, ring D without corners
-    static constexpr int npos(int r) { return 2 * (kTK + 2 * (r - 1)) + 2 * (TJ + 2 * (r - (r == D ? 1 : 0))); }
+    // positions of "ring" r: rings 1..D-2 whole, D-1 without corners, D = the 4 corners of ring
+    // D-1 plus ring D without corners (staging only)
+    static constexpr int npos(int r) {
+        return 2 * (kTK + 2 * (r - 1)) + 2 * (TJ + 2 * (r - (r >= D - 1 ? 1 : 0))) + (r == D ? 4 : 0);
+    }
     static constexpr int first(int r) { return r <= 1 ? 0 : first(r - 1) + npos(r - 1); }
     static constexpr int nall = first(D + 1);
     // ring of ring position q (D + 1: none)
@@ -208,6 +217,9 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(1,
         if (lo - flo <= fhi - hi) flo = hi + 1;
         else fhi = lo - 1;
     };
+    // ... and inside the error planes [ei0, ei1] (the periodic x planes 0 and N are outside), so
+    // the steady-state body takes the errors of every plane without a range test
+    flo = max(flo, p.ei0 + D - 1), fhi = min(fhi, p.ei1 + D - 1);
     cut(p.an_i, p.an_i + D - 2);
     cut(p.ap_i, p.ap_i + D - 2);
 #pragma unroll
@@ -237,7 +249,18 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(1,
         int g = 0, rj = jt, rk = kb;
 #pragma unroll
         for (int d = 1; d <= D; ++d)
-            if (g == 0 && q < Gm::first(d + 1)) g = d, ring(d, d == D ? 1 : 0, q - Gm::first(d), rj, rk);
+            if (g == 0 && q < Gm::first(d + 1)) {
+                g = d;
+                const int idx = q - Gm::first(d);
+                if (d < D) {
+                    ring(d, d == D - 1 ? 1 : 0, idx, rj, rk);
+                } else if (idx < 4) {  // corner of ring D-1
+                    rj = (idx & 1) ? jt + TJ - 1 + (D - 1) : jt - (D - 1);
+                    rk = (idx & 2) ? kb + kTK - 1 + (D - 1) : kb - (D - 1);
+                } else {
+                    ring(D, 1, idx - 4, rj, rk);
+                }
+            }
         rg[s] = g;
         ry[s] = rj - jt + D, rx[s] = rk - kb + D;
         rcd[s] = g != 0 && g < D && incd(rj, rk);
@@ -470,7 +493,7 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(1,
         const int e = i - (D - 1);
         if (FAST || (e >= ib && e <= ie)) {
             constexpr int HE = (P + 4 - (D - 1)) & 1;  // table row slot of plane e
-            const bool eplane = e >= p.ei0 && e <= p.ei1;
+            const bool eplane = FAST || (e >= p.ei0 && e <= p.ei1);
             T fb[R];
 #pragma unroll
             for (int r = 0; r < R; ++r) fb[r] = tq[HE][r][0] * otz;  // (sx sy) sz
@@ -478,7 +501,7 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(1,
             if constexpr (FM) {
                 const T em = eplane ? T(1) : T(0);
 #pragma unroll
-                for (int r = 0; r < R; ++r) m[r] = om[r] * em, wq[r] = tq[HE][r][NQ - 1] * ortz;
+                for (int r = 0; r < R; ++r) m[r] = FAST ? om[r] : om[r] * em, wq[r] = tq[HE][r][NQ - 1] * ortz;
             }
             sfor<D>([&](auto lc) {
                 constexpr int l = decltype(lc)::value;
@@ -516,21 +539,41 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(1,
         load_row(Ic<(P + 4 - (D - 1) + 1) & 1>{}, e + 1);
     };
 
-    auto step = [&](auto phase, const int i) {
-        if (i < flo || i > fhi) plane(phase, std::true_type{}, i);  // seam / wrap / ends
-        else plane(phase, std::false_type{}, i);
+    // i = i0 .. ie + D - 1 in three loops, each unrolled by 4 from phase 0 so every slot index
+    // is a constant: the checked body (ALIAS: seam / wrap / work-item ends) up to the first
+    // phase-0 plane of the steady window, the steady body over whole groups of 4 inside it, the
+    // checked body for the rest. One loop choosing the body per plane kept every value of the
+    // checked body live through the steady one: 337 SGPR spills and 249 VGPRs at D = 4, against
+    // none and 196 for the steady body alone.
+    const int iend = ie + D - 1;
+    const int fstart = __builtin_amdgcn_readfirstlane(i0 + ((max(flo, i0) - i0 + 3) & ~3));
+    const int fend = __builtin_amdgcn_readfirstlane(fstart + ((fhi - fstart + 1) > 0 ? ((fhi - fstart + 1) & ~3) : 0));
+    auto checked = [&](int& i, const int stop) {  // i = i0 mod 4 on entry; runs while i < stop
+        if (i >= stop) return;
+        for (;;) {
+            plane(Ph<0>{}, std::true_type{}, i);
+            if (++i >= stop) break;
+            plane(Ph<1>{}, std::true_type{}, i);
+            if (++i >= stop) break;
+            plane(Ph<2>{}, std::true_type{}, i);
+            if (++i >= stop) break;
+            plane(Ph<3>{}, std::true_type{}, i);
+            if (++i >= stop) break;
+        }
     };
-
-    // i = i0 .. ie + D - 1, unrolled by 4 so every slot index is a constant
-    for (int i = i0;;) {
-        step(Ph<0>{}, i);
-        if (++i > ie + D - 1) break;
-        step(Ph<1>{}, i);
-        if (++i > ie + D - 1) break;
-        step(Ph<2>{}, i);
-        if (++i > ie + D - 1) break;
-        step(Ph<3>{}, i);
-        if (++i > ie + D - 1) break;
+    int i = i0;
+    // one instance of the checked body: pass 0 runs it up to the steady window, then the steady
+    // loop; pass 1 runs it to the end
+#pragma nounroll
+    for (int pass = 0; pass < 2; ++pass) {
+        checked(i, pass == 0 ? min(fstart, iend + 1) : iend + 1);
+        if (pass == 0)
+            for (; i < fend; i += 4) {
+                plane(Ph<0>{}, std::false_type{}, i);
+                plane(Ph<1>{}, std::false_type{}, i + 1);
+                plane(Ph<2>{}, std::false_type{}, i + 2);
+                plane(Ph<3>{}, std::false_type{}, i + 3);
+            }
     }
     sfor<D>([&](auto lc) {
         constexpr int l = decltype(lc)::value;
@@ -556,6 +599,10 @@ int tbn_deep() {
 template <class T, int D, bool F>
 static void (*tbn_kernel(int rows, int waves, bool fm, int deep))(const TbnParams<T>) {
     if (rows != 2 || waves != 8) return nullptr;
+#ifdef W3D_TBN_ONLY  // codegen experiments: one instantiation (fp64, fma, not first, DEEP 0)
+    if constexpr (std::is_same_v<T, double> && !F && D == W3D_TBN_ONLY) return fm && deep == 0 ? k_tbn<T, D, F, 2, 8, true, 0> : nullptr;
+    else return nullptr;
+#else
     if (!fm) return deep == kTbnDeep ? k_tbn<T, D, F, 2, 8, false, kTbnDeep> : nullptr;
     if constexpr (std::is_same_v<T, double>) {
         switch (deep) {
@@ -567,6 +614,7 @@ static void (*tbn_kernel(int rows, int waves, bool fm, int deep))(const TbnParam
         }
     }
     return deep == kTbnDeep ? k_tbn<T, D, F, 2, 8, true, kTbnDeep> : nullptr;
+#endif
 }
 
 template <class T, bool F>
