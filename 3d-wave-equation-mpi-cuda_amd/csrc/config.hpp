@@ -58,7 +58,7 @@ struct Config {
     int checkpoint_every = 0;
     std::string checkpoint_dir;
     std::string resume_dir;
-    std::string kernel = "auto";    // auto | march | naive | tb2
+    std::string kernel = "auto";    // auto | march* | naive | flat | tb2* | tb3* | tbn3 | tb4 (usage())
     int chunk = 0;                  // i-planes per marching work item (0 = auto)
     int repeat = 1;                 // timed solves (benchmark mode)
     int warmup = 0;                 // untimed solves before the timed ones

@@ -39,6 +39,12 @@
 #endif
 // LDS row pitch padding (doubles/floats added to the even tile widths): 1 makes the pitches odd,
 // so a ring column (lanes at one k, consecutive rows) hits 32 distinct ds_read_b64 bank pairs
+#ifndef W3D_TB3_SPLIT  // A/B: 0 = one loop choosing the plane body per plane
+#define W3D_TB3_SPLIT 1
+#endif
+#ifndef W3D_TB3_MASKMUL  // A/B: fp64 face masks and the fma checksum as products (cmask)
+#define W3D_TB3_MASKMUL 1
+#endif
 #ifndef W3D_TB3_PAD
 #define W3D_TB3_PAD 0
 #endif
@@ -192,6 +198,16 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WP
     T om[R];  // --math fma: 1 on valid own nodes, 0 on masked lanes (branch-free errors)
 #pragma unroll
     for (int r = 0; r < R; ++r) om[r] = ovalid[r] ? T(1) : T(0);
+    // Dirichlet-face masks of computed values: a select, or (W3D_TB3_MASKMUL, fp64) a product
+    // with a 0/1 register — one op instead of two v_cndmask, and no lane masks held in SGPRs
+    constexpr bool MM = W3D_TB3_MASKMUL && sizeof(T) == 8;
+    T ocm[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) ocm[r] = ocd[r] ? T(1) : T(0);
+    auto cmask = [&](bool keep, T m, T v) {
+        if constexpr (MM) return v * m;
+        else return keep ? v : T(0);
+    };
     // self-wrap ranges of D / E met by this work item (wave-uniform bits, one test per plane)
     int rare = 0;
 #pragma unroll
@@ -245,6 +261,9 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WP
         ra_off[s] = boff(rj, rk, g != 0 && inb(rj, rk));
         rb_off[s] = boff(rj, rk, !FIRST && rcd[s] && inb(rj, rk));
     }
+    T rcm[RP];
+#pragma unroll
+    for (int s = 0; s < RP; ++s) rcm[s] = rcd[s] ? T(1) : T(0);
 
     // slots (iteration i = ib - 2 + q, phase P = q & 3):
     //   A(x), ring A(x): (x - ib + 3) & 3  -> A(i-1) = P, A(i) = P+1, A(i+1) = P+2, A(i+2) = P+3
@@ -375,7 +394,8 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WP
 #endif
 #pragma unroll
         for (int r = 0; r < R; ++r) {
-            chk += ovalid[r] ? v[r] : T(0);
+            if constexpr (MM) chk = fma_t(v[r], om[r], chk);
+            else chk += ovalid[r] ? v[r] : T(0);
             const T dv = (v[r] - fb[r] * ct) * m[r];
             ma = max_abs(ma, dv);
             mr.add(dv, wq[r]);
@@ -486,10 +506,10 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WP
             const T lap = lapA(H0, y, x, a[S1][r], xpA[r], xnA[r]);
             if constexpr (DELTA) {
                 const T dv = FIRST ? scaled(0, lap) : incr(0, bb[BC][r], lap);
-                dm[H0][r] = ocd[r] ? dv : T(0);
-                c[S0][r] = ocd[r] ? a[S1][r] + dv : T(0);  // FIRST: = taylor_first
+                dm[H0][r] = cmask(ocd[r], ocm[r], dv);
+                c[S0][r] = cmask(ocd[r], ocm[r], a[S1][r] + dv);  // FIRST: = taylor_first
             } else {
-                c[S0][r] = ocd[r] ? cval(a[S1][r], bb[BC][r], lap) : T(0);
+                c[S0][r] = cmask(ocd[r], ocm[r], cval(a[S1][r], bb[BC][r], lap));
             }
             ldsC[H0][y - 1][x - 1] = c[S0][r];
         }
@@ -500,10 +520,10 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WP
                 T cv;
                 if constexpr (DELTA) {
                     const T dv = FIRST ? scaled(0, lap) : incr(0, rb[s][BC], lap);
-                    rdm[s][H0] = rcd[s] ? dv : T(0);
-                    cv = rcd[s] ? ra[s][S1] + dv : T(0);
+                    rdm[s][H0] = cmask(rcd[s], rcm[s], dv);
+                    cv = cmask(rcd[s], rcm[s], ra[s][S1] + dv);
                 } else {
-                    cv = rcd[s] ? cval(ra[s][S1], rb[s][BC], lap) : T(0);
+                    cv = cmask(rcd[s], rcm[s], cval(ra[s][S1], rb[s][BC], lap));
                 }
                 rc[s][S0] = cv;
                 ldsC[H0][ry[s] - 1][rx[s] - 1] = cv;
@@ -534,10 +554,10 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WP
                                 ldsC[H1][y][x - 1], ldsC[H1][y][x + 1]);
                 if constexpr (DELTA) {
                     const T d1 = incr(1, dm[H1][r], l);  // d^{m+1}
-                    dm1[H0][r] = ocd[r] ? d1 : T(0);
-                    d[S0][r] = ocd[r] ? c[S3][r] + d1 : T(0);
+                    dm1[H0][r] = cmask(ocd[r], ocm[r], d1);
+                    d[S0][r] = cmask(ocd[r], ocm[r], c[S3][r] + d1);
                 } else {
-                    d[S0][r] = ocd[r] ? leap(1, c[S3][r], a[S0][r], l) : T(0);
+                    d[S0][r] = cmask(ocd[r], ocm[r], leap(1, c[S3][r], a[S0][r], l));
                 }
                 ldsD[H0][y - 1][x - 1] = d[S0][r];
             }
@@ -548,9 +568,9 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WP
                     const T l = lap(1, rc[s][S3], rcp[s], rcn[s], ldsC[H1][y - 1][x], ldsC[H1][y + 1][x],
                                     ldsC[H1][y][x - 1], ldsC[H1][y][x + 1]);
                     if constexpr (DELTA)
-                        ldsD[H0][y - 1][x - 1] = rcd[s] ? rc[s][S3] + incr(1, rdm[s][H1], l) : T(0);
+                        ldsD[H0][y - 1][x - 1] = cmask(rcd[s], rcm[s], rc[s][S3] + incr(1, rdm[s][H1], l));
                     else
-                        ldsD[H0][y - 1][x - 1] = rcd[s] ? leap(1, rc[s][S3], ra[s][S0], l) : T(0);
+                        ldsD[H0][y - 1][x - 1] = cmask(rcd[s], rcm[s], leap(1, rc[s][S3], ra[s][S0], l));
                 }
             }
             if (FAST || (id >= ib && id <= ie)) {
@@ -620,6 +640,41 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WP
         load_row(H1, i - 1);
     };
 
+#if W3D_TB3_SPLIT
+    // i = ib-2 .. ie+2 (>= 5 planes) in three loops, each unrolled by 4 from phase 0 so every
+    // slot index is a constant: the checked body (ALIAS: seam / wrap / work-item ends) up to the
+    // first phase-0 plane of the steady window [flo, fhi], the steady body over whole groups of 4
+    // inside it, the checked body for the rest. Choosing the body per plane in one loop keeps the
+    // checked body's values live through the steady one (SGPR spills: hip_tbn.hip, same split).
+    const int i0 = ib - 2, iend = ie + 2;
+    const int fstart = __builtin_amdgcn_readfirstlane(i0 + ((max(flo, i0) - i0 + 3) & ~3));
+    const int fend = __builtin_amdgcn_readfirstlane(fstart + (fhi >= fstart ? (fhi - fstart + 1) & ~3 : 0));
+    auto checked = [&](int& i, const int stop) {  // i = i0 mod 4 on entry; runs while i < stop
+        if (i >= stop) return;
+        for (;;) {
+            plane(Ph<0>{}, std::true_type{}, i);
+            if (++i >= stop) break;
+            plane(Ph<1>{}, std::true_type{}, i);
+            if (++i >= stop) break;
+            plane(Ph<2>{}, std::true_type{}, i);
+            if (++i >= stop) break;
+            plane(Ph<3>{}, std::true_type{}, i);
+            if (++i >= stop) break;
+        }
+    };
+    int i = i0;
+#pragma nounroll
+    for (int pass = 0; pass < 2; ++pass) {
+        checked(i, pass == 0 ? min(fstart, iend + 1) : iend + 1);
+        if (pass == 0 && i == fstart)
+            for (; i < fend; i += 4) {
+                plane(Ph<0>{}, std::false_type{}, i);
+                plane(Ph<1>{}, std::false_type{}, i + 1);
+                plane(Ph<2>{}, std::false_type{}, i + 2);
+                plane(Ph<3>{}, std::false_type{}, i + 3);
+            }
+    }
+#else
     auto step = [&](auto phase, const int i) {
         if (i < flo || i > fhi) plane(phase, std::true_type{}, i);  // seam / wrap / ends
         else plane(phase, std::false_type{}, i);
@@ -636,6 +691,7 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WP
         step(Ph<3>{}, i);
         if (++i > ie + 2) break;
     }
+#endif
     auto rel = [&](const Rel& m, int L) {
         if constexpr (FM) return m.value(p.ict[L]);
         else return m.value();

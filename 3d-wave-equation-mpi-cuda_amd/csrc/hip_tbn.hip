@@ -44,6 +44,10 @@
 
 #include "device_common.hpp"
 
+#ifndef W3D_TBN_MASKMUL  // A/B: face masks and the fma checksum as products (see cmask)
+#define W3D_TBN_MASKMUL 1
+#endif
+
 namespace wave3d {
 namespace {
 
@@ -314,6 +318,17 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(1,
         }
     }
 
+    // Dirichlet-face masks of the computed values: a select (two v_cndmask per double) or, with
+    // W3D_TBN_MASKMUL, a product with a 0/1 register (one op; a face value may become -0)
+    T ocm[R], rcm[RP];
+#pragma unroll
+    for (int r = 0; r < R; ++r) ocm[r] = ocd[r] ? T(1) : T(0);
+#pragma unroll
+    for (int s = 0; s < RP; ++s) rcm[s] = rcd[s] ? T(1) : T(0);
+    auto cmask = [&](bool keep, T m, T v) {
+        if constexpr (W3D_TBN_MASKMUL) return v * m;
+        else return keep ? v : T(0);
+    };
     using Rel = std::conditional_t<FM, RelMax<T>, RelArg<T>>;  // fma: |d| * 1/|f| max
     T ma[D], chk[D];
     Rel mr[D];
@@ -428,9 +443,13 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(1,
                     if (x == p.an_i) xp = bld<T>(lrs(p.nP[l]), oa[r]);
                     if (x == p.ap_i) xm = bld<T>(lrs(p.pP[l]), oa[r]);
                 }
-                const T lp = lap(lc, ctr, xm, xp, L(lc, Ic<HS>{}, y - 1, xx), L(lc, Ic<HS>{}, y + 1, xx),
-                                 L(lc, Ic<HS>{}, y, xx - 1), L(lc, Ic<HS>{}, y, xx + 1));
-                v[r] = ocd[r] ? upd(lc, ctr, pw, lp) : T(0);
+                // j neighbours inside the wave's R rows come from registers (the same values
+                // as the staged tile), only the outer two from LDS
+                auto ctr_of = [&](int q) { return l == 0 ? a[S1][q] : u[l > 0 ? l - 1 : 0][S3][q]; };
+                const T ym = r > 0 ? ctr_of(r - 1) : L(lc, Ic<HS>{}, y - 1, xx);
+                const T yp = r < R - 1 ? ctr_of(r + 1) : L(lc, Ic<HS>{}, y + 1, xx);
+                const T lp = lap(lc, ctr, xm, xp, ym, yp, L(lc, Ic<HS>{}, y, xx - 1), L(lc, Ic<HS>{}, y, xx + 1));
+                v[r] = cmask(ocd[r], ocm[r], upd(lc, ctr, pw, lp));
                 if constexpr (l <= D - 2) {
                     u[l][S0][r] = v[r];
                     L(Ic<l + 1>{}, Ic<H0>{}, y, xx) = v[r];
@@ -458,7 +477,7 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(1,
                             const int y = ry[s], xx = rx[s];
                             const T lp = lap(lc, ctr, xm, xp, L(lc, Ic<HS>{}, y - 1, xx), L(lc, Ic<HS>{}, y + 1, xx),
                                              L(lc, Ic<HS>{}, y, xx - 1), L(lc, Ic<HS>{}, y, xx + 1));
-                            const T cv = rcd[s] ? upd(lc, ctr, pw, lp) : T(0);
+                            const T cv = cmask(rcd[s], rcm[s], upd(lc, ctr, pw, lp));
                             if constexpr (l <= D - 3) ru[s][l][S0] = cv;
                             L(Ic<l + 1>{}, Ic<H0>{}, y, xx) = cv;
                         }
@@ -515,7 +534,8 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(1,
                 if constexpr (FM) {
 #pragma unroll
                     for (int r = 0; r < R; ++r) {
-                        chk[l] += ovalid[r] ? val[r] : T(0);
+                        if constexpr (W3D_TBN_MASKMUL) chk[l] = fma_t(val[r], om[r], chk[l]);
+                        else chk[l] += ovalid[r] ? val[r] : T(0);
                         const T dv = (val[r] - fb[r] * p.ct[l]) * m[r];
                         ma[l] = max_abs(ma[l], dv);
                         mr[l].add(dv, wq[r]);
@@ -547,7 +567,8 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(1,
     // none and 196 for the steady body alone.
     const int iend = ie + D - 1;
     const int fstart = __builtin_amdgcn_readfirstlane(i0 + ((max(flo, i0) - i0 + 3) & ~3));
-    const int fend = __builtin_amdgcn_readfirstlane(fstart + ((fhi - fstart + 1) > 0 ? ((fhi - fstart + 1) & ~3) : 0));
+    // whole groups of 4 steady planes from fstart (none when the window is shorter)
+    const int fend = __builtin_amdgcn_readfirstlane(fstart + (fhi >= fstart ? (fhi - fstart + 1) & ~3 : 0));
     auto checked = [&](int& i, const int stop) {  // i = i0 mod 4 on entry; runs while i < stop
         if (i >= stop) return;
         for (;;) {
@@ -567,7 +588,7 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(1,
 #pragma nounroll
     for (int pass = 0; pass < 2; ++pass) {
         checked(i, pass == 0 ? min(fstart, iend + 1) : iend + 1);
-        if (pass == 0)
+        if (pass == 0 && i == fstart)  // (a work item shorter than the window start ran through)
             for (; i < fend; i += 4) {
                 plane(Ph<0>{}, std::false_type{}, i);
                 plane(Ph<1>{}, std::false_type{}, i + 1);
@@ -598,22 +619,29 @@ int tbn_deep() {
 
 template <class T, int D, bool F>
 static void (*tbn_kernel(int rows, int waves, bool fm, int deep))(const TbnParams<T>) {
-    if (rows != 2 || waves != 8) return nullptr;
-#ifdef W3D_TBN_ONLY  // codegen experiments: one instantiation (fp64, fma, not first, DEEP 0)
-    if constexpr (std::is_same_v<T, double> && !F && D == W3D_TBN_ONLY) return fm && deep == 0 ? k_tbn<T, D, F, 2, 8, true, 0> : nullptr;
+#ifdef W3D_TBN_ONLY  // codegen experiments: one instantiation (fp64, fma, not first, default DEEP)
+#ifndef W3D_TBN_PROBE_R
+#define W3D_TBN_PROBE_R 2
+#define W3D_TBN_PROBE_NW 8
+#endif
+    constexpr int PR = W3D_TBN_PROBE_R, PW = W3D_TBN_PROBE_NW;
+    if constexpr (std::is_same_v<T, double> && !F && D == W3D_TBN_ONLY)
+        return fm && deep == kTbnDeep && rows == PR && waves == PW ? k_tbn<T, D, F, PR, PW, true, kTbnDeep> : nullptr;
     else return nullptr;
 #else
-    if (!fm) return deep == kTbnDeep ? k_tbn<T, D, F, 2, 8, false, kTbnDeep> : nullptr;
-    if constexpr (std::is_same_v<T, double>) {
-        switch (deep) {
-            case 0: return k_tbn<T, D, F, 2, 8, true, 0>;
-            case 1: return k_tbn<T, D, F, 2, 8, true, 1>;
-            case 2: return k_tbn<T, D, F, 2, 8, true, 2>;
-            case 3: return k_tbn<T, D, F, 2, 8, true, 3>;
-            default: return nullptr;
-        }
-    }
-    return deep == kTbnDeep ? k_tbn<T, D, F, 2, 8, true, kTbnDeep> : nullptr;
+#ifdef W3D_TBN_DEEP_VARIANTS  // load-pipeline A/B (fp64 --math fma): WAVE3D_TBN_DEEP = 0..3
+    if constexpr (std::is_same_v<T, double>)
+        if (fm && rows == 2 && waves == 8) switch (deep) {
+                case 0: return k_tbn<T, D, F, 2, 8, true, 0>;
+                case 1: return k_tbn<T, D, F, 2, 8, true, 1>;
+                case 2: return k_tbn<T, D, F, 2, 8, true, 2>;
+                case 3: return k_tbn<T, D, F, 2, 8, true, 3>;
+                default: return nullptr;
+            }
+#endif
+    if (deep != kTbnDeep) return nullptr;
+    if (rows == 2 && waves == 8) return fm ? k_tbn<T, D, F, 2, 8, true, kTbnDeep> : k_tbn<T, D, F, 2, 8, false, kTbnDeep>;
+    return nullptr;
 #endif
 }
 

@@ -29,27 +29,32 @@ static void parse_tb(const std::string& name, int& rows, int& waves, int& occ, i
 
 Layout plan_layout(const Config& c, int world) {
     Layout l;
-    // "auto": temporal blocking (tb2, measured fastest on MI355X, profiles/). The process
+    // "auto": temporal blocking (the measured fastest sweep per dtype / scheme / math, below). The process
     // grid is MPI_Dims_create's as in the reference (2x2x2 at 8 ranks; y/z splits get 2-deep
     // row/column halos); `--dims P,1,1` selects x slabs (contiguous planes, 2 peers)
     const bool auto_tb = c.kernel == "auto";
     // fp32: three-layer blocking (tb3r2w8, 4 waves per SIMD after the register diet) moves
     // 10.7 instead of 16 B per node-layer and beats tb2r2w8 by 12-14 % (leapfrog) / 3-4 %
-    // (increment form), N=512 / 2048 (profiles/tb3_diet_r2.txt); fp64 stays on tb2
+    // (increment form), N=512 / 2048 (profiles/tb3_diet_r2.txt)
     // fp64 with --math fma: three-layer blocking too — the FMA form cuts the issue-bound fp64
     // sweep's VALU work (profiles/math_fma_r3.txt). After the scalar diet (steady-state body,
     // errors of three layers per table row) the 16-row r2w8 tile (2 waves/SIMD) beats the
     // 1-row r1w8 (4 waves/SIMD): 425-431k vs 402k Mpts/s at N=512 (profiles/tb3_salu_r3.txt)
     // fp64 exact leapfrog: tb3 too since the scalar diet — 373-374k vs tb2r2w8 317k Mpts/s at
     // N=512, bitwise equal (profiles/tb3_salu_r3.txt); the fp64 increment form stays on tb2r2w4
-    const bool auto_tb3 = auto_tb && (c.dtype == DType::F32 || c.fma || !c.delta);
+    // Since round 4 the leapfrog (fp64 and fp32, exact and FMA) runs four layers per sweep (tb4,
+    // k_tbn r2w8: 8 B per node-layer instead of 10.7): fp64 fma 521-528k vs tb3 428-435k, exact
+    // 433k vs 374k, fp32 fma 794k vs 791k, fp32 exact 825k vs 717k Mpts/s at N=512 K=100
+    // (profiles/deep_sweeps_r4.txt). k_tbn has no increment form: fp32 / fp64-fma delta stay on tb3.
+    const bool auto_tb4 = auto_tb && !c.delta;
+    const bool auto_tb3 = auto_tb && !auto_tb4 && (c.dtype == DType::F32 || c.fma);
     const bool tbn3 = c.kernel.rfind("tbn3", 0) == 0;  // k_tbn at depth 3 (A/B of k_tb3)
-    const bool tb4 = c.kernel.rfind("tb4", 0) == 0;
+    const bool tb4 = auto_tb4 || c.kernel.rfind("tb4", 0) == 0;
     const bool tb3 = !tb4 && (auto_tb3 || tbn3 || c.kernel.rfind("tb3", 0) == 0);
     l.generic = tb4 || tbn3;
     l.tb = auto_tb || tb3 || tb4 || c.kernel.rfind("tb2", 0) == 0;
     l.depth = tb4 ? 4 : (tb3 ? 3 : (l.tb ? 2 : 1));
-    if (tb3 || tb4) l.rows = 2, l.waves = 8;  // measured best three-layer tile (profiles/)
+    if (tb3 || tb4) l.rows = 2, l.waves = 8;  // measured best deep-sweep tile (profiles/)
     // 16-row tiles of 8 waves (tb2r2w8, 2 workgroups per CU): fp64 +2-3 % over r2w4 (128
     // VGPRs, 4 waves/SIMD), fp32 +3.5 % (N=512) / +5 % (N=2048) over tb2r4 (profiles/
     // ab_tiles_r2.txt, fp32_accuracy_r2.txt). The fp64 increment form needs a few more

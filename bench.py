@@ -16,9 +16,10 @@ the reference (the reference's errors are identical for every P
     8 GPUs: N=1024, 2x2x2 blocks   (config 4)      golden 8.04265e-08   weak vs 1 GPU
 
 The decomposition is MPI_Dims_create's, as in the reference (mpi_new.cpp:409-433); `--dims`
-overrides it. The default kernel is three-layer temporal blocking (tb3: 3 layers per sweep,
-~10.7 instead of 24 B/node/layer, 4 time levels) with 3-deep RCCL halos; `--kernel tb2` selects
-two-layer blocking, `--kernel march2` the single-step kernel.
+overrides it. The default kernel is four-layer temporal blocking (tb4: 4 layers per sweep,
+~8 instead of 24 B/node/layer, 4 time levels) with 4-deep RCCL halos; the fp32 increment form
+runs three layers per sweep (tb3); `--kernel tb3|tb2` selects three- / two-layer blocking,
+`--kernel march2` the single-step kernel.
 The JSON line states what ran: N and dtype in the metric, dims, the effective overlap,
 the transport and the ranks RCCL itself reports (ncclCommCount), and whether the L-inf
 matches the golden. Data: the analytic initial condition on a synthetic grid (the

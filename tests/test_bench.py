@@ -103,7 +103,7 @@ def test_bench_gpu_default_config_short():
     r = _bench(["--steps", "1", "--warmup", "1"])
     _check(r, 1, 1, 1)
     assert r["scaling"] == "weak" and r["config"]["N"] == 512 and r["config"]["timesteps"] == 100
-    assert r["math"] == "fma" and r["config"]["kernel"] == "tb3"  # the GPU default (presets)
+    assert r["math"] == "fma" and r["config"]["kernel"] == "tb4"  # the GPU default (presets)
     assert f"{r['linf_abs']:.6g}" == "6.03381e-07"  # golden N=512 K=100
     assert r["linf_golden"] == 6.03381e-07 and r["linf_ok"] is True
     assert r["config"]["dims"] == [1, 1, 1] and r["config"]["overlap"] is False  # no remote halo
@@ -152,7 +152,8 @@ def test_bench_gpu_fp32_two_ranks_staged(scheme, linf):
     r = _bench(["--steps", "1", "--warmup", "0", "--dtype", "fp32", "--transport", "staged",
                 "--shared-device", "--overlap", "on", "--scheme", scheme, "--math", "exact"], nproc=2, timeout=600)
     assert r["dtype"] == "fp32" and r["n_gpus"] == 2 and r["config"]["dims"] == [2, 1, 1]
-    assert r["config"]["kernel"] == "tb3" and r["config"]["overlap"] is True
+    # the leapfrog runs four layers per sweep (tb4), the increment form three (tb3)
+    assert r["config"]["kernel"] == ("tb3" if scheme == "auto" else "tb4") and r["config"]["overlap"] is True
     assert r["scheme"] == ("delta" if scheme == "auto" else scheme)
     assert f"{r['linf_abs']:.6g}" == linf
     assert f"{r['linf_fp64_ref']:.6g}" == "6.03381e-07"

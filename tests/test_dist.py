@@ -74,11 +74,11 @@ def test_hip_multiprocess_temporal_blocking(C, single_cpu, P, kernel):
 @pytest.mark.parametrize("P,dims,kernel", [(8, "2,2,2", "auto"), (4, "1,2,2", "tb2r2w8")])
 def test_hip_multiprocess_temporal_blocking_3d(C, single_cpu, P, dims, kernel):
     """Temporal blocking on the reference's 3-D block decomposition (6-face deep halos), P
-    processes through the tag-less FIFO staged transport: the fp64 auto kernel (tb3) and tb2."""
+    processes through the tag-less FIFO staged transport: the fp64 auto kernel (tb4) and tb2."""
     r = torchrun(P, ["--backend", "hip", "--transport", "staged", "--shared-device"],
                  ARGS + ["--dims", dims, "--kernel", kernel])
     assert r["dims"] == [int(x) for x in dims.split(",")]
-    assert r["kernel"] == {"auto": "tb3"}.get(kernel, kernel)  # fp64 auto = tb3
+    assert r["kernel"] == {"auto": "tb4"}.get(kernel, kernel)  # fp64 auto = tb4
     assert r["max_abs"] == single_cpu["max_abs"] and r["max_rel"] == single_cpu["max_rel"]
 
 

@@ -27,7 +27,7 @@ def test_golden_n32(C, kernel):
     from wave3d.utils import GOLDEN_N32_K20
 
     r = _solve(wave3d.WaveProblem(32, timesteps=20), kernel=kernel)
-    assert r.backend == "hip" and r.kernel == {"march": "march4", "auto": "tb3"}.get(kernel, kernel)
+    assert r.backend == "hip" and r.kernel == {"march": "march4", "auto": "tb4"}.get(kernel, kernel)
     assert _fmt(r) == GOLDEN_N32_K20
 
 
@@ -383,18 +383,18 @@ def test_tile_orders_bitwise(C, kernel):
     assert out["band"] == out["j"] == out["k"]
 
 
-def test_fp32_auto_is_tb3_bitwise(C):
-    """fp32 leapfrog "auto" runs three-layer blocking (tb3r2w8): bitwise equal to the OpenMP
-    fp32 oracle on one rank and on a 2x2x1 decomposition with overlap (3-deep halos)."""
+def test_fp32_auto_is_tb4_bitwise(C):
+    """fp32 leapfrog "auto" runs four-layer blocking (tb4, k_tbn r2w8): bitwise equal to the
+    OpenMP fp32 oracle on one rank and on a 2x2x1 decomposition with overlap (4-deep halos)."""
     import wave3d
 
     p = wave3d.WaveProblem(40, timesteps=13, dtype="fp32", ic="shifted")
     ref = _solve(p, "cpu")
     got = _solve(p)
-    assert got.kernel == "tb3"
+    assert got.kernel == "tb4"
     assert got.max_abs == ref.max_abs and got.max_rel == ref.max_rel
     multi = _solve(p, ranks=4, dims=[2, 2, 1], overlap=True)
-    assert multi.kernel == "tb3"
+    assert multi.kernel == "tb4"
     assert multi.max_abs == ref.max_abs and multi.max_rel == ref.max_rel
 
 

@@ -269,6 +269,9 @@ TBN_CASES = [
     ((11, 40, 131), [(1, 11, 1, 40, 1, 130)], (1, 11, 1, 40, 1, 130), 0),
     ((13, 21, 70), [(1, 2, 1, 21, 1, 69), (3, 13, 5, 9, 2, 66)], (1, 13, 1, 21, 1, 69), 5),
     ((9, 9, 11), [(1, 9, 2, 8, 2, 10)], (1, 9, 2, 8, 2, 10), 0),
+    # one- and two-plane work items: shorter than the steady window's start (only checked planes)
+    ((11, 40, 131), [(2, 10, 3, 37, 60, 130)], (1, 11, 1, 40, 1, 130), 1),
+    ((11, 40, 131), [(1, 11, 1, 40, 1, 130)], (1, 11, 1, 40, 1, 130), 2),
 ]
 
 

@@ -10,7 +10,7 @@ ARGS = ["512", "1", "pi", "pi", "pi", "1", "100"]
 
 def test_layout_auto_is_temporal_blocking_on_dims_create(C):
     p1 = C.memory_plan(ARGS, 1)
-    assert p1["tb"] and p1["ghost"] == 3 and p1["levels"] == 4  # fp64 auto = tb3, 4-level ring
+    assert p1["tb"] and p1["ghost"] == 4 and p1["levels"] == 4  # fp64 auto = tb4, 4-level ring
     p8 = C.memory_plan(ARGS, 8)  # no override: MPI_Dims_create's 2x2x2, as the reference
     assert p8["tb"] and p8["dims"] == [0, 0, 0]
     s8 = C.memory_plan(ARGS + ["--dims", "8,1,1"], 8)  # x slabs on request
@@ -22,22 +22,23 @@ def test_layout_auto_is_temporal_blocking_on_dims_create(C):
 
 
 def test_bytes_per_rank_matches_level_formula(C):
-    # one rank, N=512 fp64, three-layer blocking (tb3): 4 levels of (513+6)^2 x
-    # roundup(16+513+3, 16)
-    sj = ((16 + 513 + 3 + 15) // 16) * 16
-    level = (513 + 6) * (513 + 6) * sj * 8
+    # one rank, N=512 fp64, four-layer blocking (tb4): 4 levels of (513+8)^2 x
+    # roundup(16+513+4, 16)
+    sj = ((16 + 513 + 4 + 15) // 16) * 16
+    level = (513 + 8) * (513 + 8) * sj * 8
     b = C.memory_plan(ARGS, 1)["bytes_per_rank"]
     assert 4 * level <= b < 4 * level * 1.01
-    # fp32 halves the level size (rows padded to 32 elements); also tb3: 4 levels, 3-deep ghosts
-    p32 = C.memory_plan(ARGS + ["--dtype", "fp32"], 1)
-    assert p32["tb"] and p32["ghost"] == 3 and p32["levels"] == 4
+    # fp32 halves the level size (rows padded to 32 elements); leapfrog also tb4: 4 levels, 4-deep
+    p32 = C.memory_plan(ARGS + ["--dtype", "fp32", "--scheme", "leapfrog"], 1)
+    assert p32["tb"] and p32["ghost"] == 4 and p32["levels"] == 4
     b32 = p32["bytes_per_rank"]
     assert 0.50 * b < b32 < 0.56 * b
     # the fp64 increment form keeps two-layer blocking (4 levels, 2-deep ghosts)
     pd = C.memory_plan(ARGS + ["--scheme", "delta"], 1)
     assert pd["ghost"] == 2 and pd["levels"] == 4
-    p32d = C.memory_plan(ARGS + ["--dtype", "fp32", "--scheme", "delta"], 1)  # increment form too
-    assert p32d["ghost"] == 3 and p32d["levels"] == 4 and p32d["bytes_per_rank"] == b32
+    # the fp32 increment form: three-layer blocking (tb3, no tb4 increment form), 3-deep ghosts
+    p32d = C.memory_plan(ARGS + ["--dtype", "fp32", "--scheme", "delta"], 1)
+    assert p32d["ghost"] == 3 and p32d["levels"] == 4 and p32d["bytes_per_rank"] < b32
     assert C.memory_plan(ARGS, 8)["bytes_per_rank"] < b / 7
 
 
@@ -48,7 +49,7 @@ def test_fill_hbm_is_tight(C, extra, world):
     N = C.fill_hbm_N(ARGS + extra, world, budget)
     at = lambda n: C.memory_plan([str(n)] + ARGS[1:] + extra, world)["bytes_per_rank"]
     assert at(N) <= budget < at(N + 1)
-    # 0.9 x 288e9 B holds ~1996^3 fp64 nodes with tb3's 4 levels (5 levels: ~1850^3); the
+    # 0.9 x 288e9 B holds ~1996^3 fp64 nodes with 4 levels (5 levels: ~1850^3); the
     # program takes the budget from hipMemGetInfo's total (288 GiB on an MI355X): ~2040^3
     assert N > 1950
 

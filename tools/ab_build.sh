@@ -1,21 +1,27 @@
 #!/bin/bash
-# Build A/B variants of one HIP source with extra compiler flags into gpurun_ab/<name>/
+# Build A/B variants of HIP sources with extra compiler flags into gpurun_ab/<name>/
 # {libwave3d.so, wave3d}, linked against the tree's other objects (make first):
 #   tools/ab_build.sh hip_tb3 "nb2:-DW3D_TB3_NB=2" "nb4:-DW3D_TB3_NB=4"
+#   tools/ab_build.sh hip_tb3,hip_tbn "noslp:-fno-slp-vectorize"
 set -e
 cd "$(dirname "$0")/../3d-wave-equation-mpi-cuda_amd"
 ROCM=/opt/rocm
 FLAGS="-O3 -std=c++17 -fPIC -ffp-contract=off -Wall -Wno-unknown-pragmas --offload-arch=gfx950 -fopenmp -munsafe-fp-atomics -I$ROCM/include -Wno-pass-failed"
-src=$1; shift
-objs=$(ls build/hip/*.o | grep -v "/$src.o\$")
+srcs=${1//,/ }; shift
+objs=$(ls build/hip/*.o)
+for src in $srcs; do objs=$(echo "$objs" | grep -v "/$src.o\$"); done
 for v in "$@"; do
   (
     name=${v%%:*}; extra=${v#*:}
     out=../gpurun_ab/$name; mkdir -p $out
-    $ROCM/bin/hipcc $FLAGS $extra -c csrc/$src.hip -o $out/$src.o
-    $ROCM/bin/hipcc -shared --offload-arch=gfx950 $objs $out/$src.o -L$ROCM/lib -lamdhip64 -lrccl \
+    vobjs=""
+    for src in $srcs; do
+      $ROCM/bin/hipcc $FLAGS $extra -c csrc/$src.hip -o $out/$src.o
+      vobjs="$vobjs $out/$src.o"
+    done
+    $ROCM/bin/hipcc -shared --offload-arch=gfx950 $objs $vobjs -L$ROCM/lib -lamdhip64 -lrccl \
         -lrocprofiler-sdk-roctx -fopenmp -Wl,-rpath,$ROCM/lib -o $out/libwave3d.so
-    rm $out/$src.o
+    rm $vobjs
     cp build/wave3d $out/
     echo "built $out"
   ) &

@@ -9,7 +9,7 @@ for rep in $(seq "$rounds"); do
     IFS=: read -r b k d <<< "$v"
     W=gpurun_ab/$b/wave3d; [ "$b" = main ] && W=3d-wave-equation-mpi-cuda_amd/build/wave3d
     echo -n "round=$rep $b $k deep=$d "
-    WAVE3D_TBN_DEEP=$d timeout -k 10 120 $W ${N:-512} 1 pi pi pi 1 ${K:-100} --math fma --kernel $k --repeat 5 --warmup 1 \
+    WAVE3D_TBN_DEEP=$d timeout -k 10 ${TMO:-120} $W ${N:-512} 1 pi pi pi 1 ${K:-100} --math fma --kernel $k --repeat ${REP:-5} --warmup 1 \
         --json --quiet --format none ${EXTRA:-} \
       | python3 -c "import sys,json; r=json.loads(sys.stdin.read().splitlines()[-1]); print(round(r['mpts_per_s_best']), '%.9g' % r['linf_abs'], r['kernel'])" || exit 1
   done
