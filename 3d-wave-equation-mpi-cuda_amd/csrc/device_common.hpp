@@ -225,8 +225,21 @@ inline int auto_chunk_boxes(int best, const int* tiles, const int* planes, int n
     return std::max(1, std::max(8, int(work / kTarget)));
 }
 
-// Resident workgroups of a sweep kernel on the whole device (CUs x occupancy), cached per kernel
-// and device (thread-per-GPU ranks launch concurrently).
+// CUs withheld from this host thread's sweep launches: while overlap is on, the compute stream
+// is CU-masked so the halo stream's kernels (RCCL, pack/unpack, shells) always find free CUs,
+// and work items are sized for the CUs it keeps (hip_solver comm_cu_reserve()).
+inline int& launch_cu_reserve() {
+    thread_local int r = 0;
+    return r;
+}
+struct CuReserveScope {
+    int old;
+    explicit CuReserveScope(int r) : old(launch_cu_reserve()) { launch_cu_reserve() = r; }
+    ~CuReserveScope() { launch_cu_reserve() = old; }
+};
+
+// Resident workgroups of a sweep kernel on the device (CUs x occupancy, less the reserved CUs),
+// cached per kernel and device (thread-per-GPU ranks launch concurrently).
 inline int resident_slots(const void* kern, int threads) {
     static std::mutex mu;
     static std::unordered_map<const void*, int> occ;
@@ -242,7 +255,8 @@ inline int resident_slots(const void* kern, int threads) {
         HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, kern, threads, 0));
         it = occ.emplace(kern, std::max(1, n)).first;
     }
-    return std::max(1, (dev >= 0 && dev < 64 ? cus[dev] : 256) * it->second);
+    const int n = dev >= 0 && dev < 64 ? cus[dev] : 256;
+    return std::max(1, std::max(1, n - launch_cu_reserve()) * it->second);
 }
 
 // Work-item length of a one-box sweep: the march pays `extra` planes of prologue/epilogue per

@@ -14,6 +14,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <cstdlib>
 #include <cstring>
 #include <iostream>
 #include <map>
@@ -21,6 +22,7 @@
 #include <thread>
 
 #include "checkpoint.hpp"
+#include "device_common.hpp"
 #include "hip_kernels.hpp"
 #include "hip_selftest.hpp"
 #include "rccl_transport.hpp"
@@ -54,6 +56,14 @@ std::string tb_name(int rows, int waves, int occ, int depth = 2, int kwaves = 1)
     if (kwaves != 1) s += "k" + std::to_string(kwaves);
     if (occ) s += "o" + std::to_string(occ);
     return s;
+}
+
+// CUs the compute stream leaves to the halo stream while overlap is on (WAVE3D_COMM_CUS,
+// default kCommCus; 0 = no CU-masked stream)
+constexpr int kCommCus = 0;
+int comm_cu_reserve() {
+    const char* e = std::getenv("WAVE3D_COMM_CUS");
+    return e && *e ? std::max(0, std::atoi(e)) : kCommCus;
 }
 
 constexpr int kMaxLevels = 4;  // time levels: 3 single-step, 4 with two- / three-layer sweeps
@@ -345,6 +355,27 @@ private:
         int prio_lo = 0, prio_hi = 0;
         HIP_CHECK(hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi));
         HIP_CHECK(hipStreamCreateWithPriority(&s_comm_, hipStreamNonBlocking, prio_hi));
+        // While overlap is on, the sweeps run on a CU-masked twin of the compute stream: an
+        // interior sweep holds one workgroup per CU for its whole march, so without a reserve the
+        // halo stream's kernels (RCCL send/recv, pack/unpack, the next shells) wait for it to
+        // drain and the exchange serialises behind it
+        s_comp_full_ = s_comp_;
+        comm_cus_ = comm_cu_reserve();
+        if (comm_cus_ > 0 && (ext_ || world_ > 1) && cfg_.overlap) {
+            int dev = 0, cus = 0;
+            HIP_CHECK(hipGetDevice(&dev));
+            HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+            comm_cus_ = std::min(comm_cus_, cus / 2);
+            // every (cus / reserve)-th CU index: spread over the shader engines and XCDs
+            std::vector<uint32_t> mask(size_t(cus + 31) / 32, 0u);
+            const int stride = cus / comm_cus_;
+            for (int c = 0; c < cus; ++c)
+                if (!(c % stride == stride - 1 && c / stride < comm_cus_)) mask[size_t(c) / 32] |= 1u << (c % 32);
+            HIP_CHECK(hipExtStreamCreateWithCUMask(&s_comp_cu_, uint32_t(mask.size()), mask.data()));
+            if (overlap_) s_comp_ = s_comp_cu_;
+        } else {
+            comm_cus_ = 0;
+        }
         HIP_CHECK(hipEventCreateWithFlags(&ev_start_, hipEventDefault));
         HIP_CHECK(hipEventCreateWithFlags(&ev_end_, hipEventDefault));
         HIP_CHECK(hipEventCreateWithFlags(&ev_layer_, hipEventDisableTiming));
@@ -537,7 +568,8 @@ private:
         if (mirror_res_) (void)hipFree(mirror_res_);
         mirror_buf_ = nullptr, mirror_res_ = nullptr;
         mirror_.reset();
-        if (s_comp_) (void)hipStreamDestroy(s_comp_);
+        if (s_comp_full_) (void)hipStreamDestroy(s_comp_full_);
+        if (s_comp_cu_) (void)hipStreamDestroy(s_comp_cu_);
         if (s_comm_) (void)hipStreamDestroy(s_comm_);
         for (auto e : {ev_start_, ev_end_, ev_layer_, ev_halo_, ev_shell_})
             if (e) (void)hipEventDestroy(e);
@@ -548,7 +580,7 @@ private:
         ts_host_ = ts_dev_ = nullptr;
         if (gexec_) (void)hipGraphExecDestroy(gexec_);
         gexec_ = nullptr;
-        s_comp_ = s_comm_ = nullptr;
+        s_comp_ = s_comm_ = s_comp_full_ = s_comp_cu_ = nullptr;
     }
 
     // ---- helpers ----------------------------------------------------------------------
@@ -556,6 +588,8 @@ private:
     void set_overlap(bool on) {
         if (on == overlap_) return;
         overlap_ = on;
+        // between solves (both streams idle): the sweeps move to the CU-masked stream and back
+        if (s_comp_cu_) s_comp_ = on ? s_comp_cu_ : s_comp_full_;
         if (gexec_) (void)hipGraphExecDestroy(gexec_);
         gexec_ = nullptr;
     }
@@ -1753,6 +1787,7 @@ private:
     // Returns the last layer computed.
     int enqueue_layers(RunResult& res, int start) {
         TraceRange tr("wave3d.layers");
+        CuReserveScope cu_scope(s_comp_ == s_comp_cu_ ? comm_cus_ : 0);  // work items for the CUs kept
         const int K = prob_.K;
         int done = start - 1;
         for (int n = start; n <= K;) {
@@ -2194,6 +2229,8 @@ private:
     int ckpt_levels_[2] = {-1, -1};
     std::vector<double> ckpt_abs_, ckpt_rel_;
     hipStream_t s_comp_ = nullptr, s_comm_ = nullptr;
+    hipStream_t s_comp_full_ = nullptr, s_comp_cu_ = nullptr;  // s_comp_ is one of them
+    int comm_cus_ = 0;  // CUs the masked compute stream leaves to the halo stream
     hipEvent_t ev_start_ = nullptr, ev_end_ = nullptr, ev_layer_ = nullptr, ev_halo_ = nullptr;
     hipEvent_t ev_shell_ = nullptr;  // shells of the current sweep done (comm stream)
     u64* ts_host_ = nullptr;       // timer-mark stamps (pinned, coherent host memory)

@@ -85,7 +85,7 @@ def test_fp32_close(C):
     assert b.max_abs[-1] == pytest.approx(a.max_abs[-1], rel=0.05)
 
 
-@pytest.mark.parametrize("kernel", ["auto", "march2"])
+@pytest.mark.parametrize("kernel", ["auto", "tb3", "march2"])
 @pytest.mark.parametrize("K", [12, 13])
 def test_checkpoint_resume(C, tmp_path, kernel, K):
     import wave3d
@@ -95,10 +95,12 @@ def test_checkpoint_resume(C, tmp_path, kernel, K):
     d = str(tmp_path)
     _solve(p, ranks=2, checkpoint_every=5, checkpoint_dir=d, kernel=kernel)
     # a checkpoint is written at the end of a sweep holding a multiple of 5 (not the last one):
-    # layer 10 for single steps; for the three-layer sweeps of the fp64 auto kernel (tb3: layers
-    # 1-3, 4-6, 7-9, 10-12, then a single step for K=13) layer 6 at K=12 and 12 at K=13
+    # layer 10 for single steps; three-layer sweeps (tb3: layers 1-3, 4-6, 7-9, 10-12, then a
+    # single step for K=13): layer 6 at K=12 and 12 at K=13; four-layer sweeps of the fp64 auto
+    # kernel (tb4: 1-4, 5-8, 9-12, then a single step for K=13): 8 at K=12 and 12 at K=13
     layers = sorted(int(f[len("ckpt_r0_L"):-4]) for f in os.listdir(d) if f.startswith("ckpt_r0_L"))
-    assert layers and layers[-1] == (10 if kernel == "march2" else (12 if K == 13 else 6))
+    want = {"march2": {12: 10, 13: 10}, "tb3": {12: 6, 13: 12}, "auto": {12: 8, 13: 12}}[kernel][K]
+    assert layers and layers[-1] == want
     res = _solve(p, ranks=2, resume=d, kernel=kernel)
     assert res.extra["resumed_from"] == layers[-1]
     assert res.max_abs == full.max_abs and res.max_rel == full.max_rel
@@ -110,8 +112,8 @@ def test_fault_detection(C):
     p = wave3d.WaveProblem(24, timesteps=10)
     r = _solve(p, check_every=1, fault="nan:0:4")
     # the NaN is written after the sweep holding layer 4 and seen by the next sweep's fused
-    # errors: layer 5 with two-layer sweeps, 7 with the three-layer sweeps of the fp64 auto (tb3)
-    assert r.aborted and 4 <= r.abort_layer <= 7
+    # errors: layer 5 with two-layer sweeps, up to 8 with the four-layer sweeps of the fp64 auto (tb4)
+    assert r.aborted and 4 <= r.abort_layer <= 8
     ok = _solve(p, check_every=1)
     assert not ok.aborted
     bad = _solve(p, ranks=2, fault="drop_face:1:4")  # an exchanged layer for tb2 and march2
