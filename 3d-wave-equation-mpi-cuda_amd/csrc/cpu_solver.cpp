@@ -241,6 +241,7 @@ private:
         // --math fma: coef/h^2 folded (stencil_math coef_lap_fma), as the HIP kernels
         const double cf = n == 1 ? prob_.coef_first : prob_.coef;
         const T fx = T(cf / prob_.hx2), fy = T(cf / prob_.hy2), fz = T(cf / prob_.hz2);
+        const T fk = fm_kc(fx, fy, fz);  // leap_fm's centre factor
         const bool fm = cfg_.fma;
         const i64 si = R.si, sj = R.sj;
         const bool first = n == 1;
@@ -259,7 +260,10 @@ private:
                         const i64 p = base + k;
                         const T c = u1[p];
                         T v;
-                        if (fm) {
+                        if (fm && !dnext && !first) {
+                            v = leap_fm(c, u2[p], u1[p - si], u1[p + si], u1[p - sj], u1[p + sj], u1[p - 1],
+                                        u1[p + 1], fx, fy, fz, fk);
+                        } else if (fm) {
                             const T l = coef_lap_fma(c, u1[p - si], u1[p + si], u1[p - sj], u1[p + sj], u1[p - 1],
                                                      u1[p + 1], fx, fy, fz);
                             if (dnext) {
@@ -267,7 +271,7 @@ private:
                                 v = c + d;
                                 dnext[p] = d;
                             } else {
-                                v = first ? c + l : leapfrog_fma(c, u2[p], l);
+                                v = c + l;  // the Taylor start
                             }
                         } else {
                             T lap = laplace7(c, u1[p - si], u1[p + si], u1[p - sj], u1[p + sj],

@@ -69,8 +69,11 @@ struct StepParams {
 template <class T, bool FIRST>
 __device__ __forceinline__ T point_update(const StepParams<T>& p, T c, T xm, T xp, T ym, T yp, T zm, T zp, i64 o) {
     if (p.fm) {
+        if (!FIRST && !p.delta)
+            return leap_fm(c, p.u2[o], xm, xp, ym, yp, zm, zp, p.fc[0], p.fc[1], p.fc[2],
+                           fm_kc(p.fc[0], p.fc[1], p.fc[2]));
         const T l = coef_lap_fma(c, xm, xp, ym, yp, zm, zp, p.fc[0], p.fc[1], p.fc[2]);
-        return FIRST ? c + l : (p.delta ? c + (p.u2[o] + l) : leapfrog_fma(c, p.u2[o], l));
+        return FIRST ? c + l : c + (p.u2[o] + l);
     }
     const T lap = laplace7_cr(c, xm, xp, ym, yp, zm, zp, p.hx2, p.hy2, p.hz2, p.yx2, p.yy2, p.yz2);
     return FIRST ? taylor_first(c, lap, p.coef)
@@ -245,10 +248,13 @@ __global__ void __launch_bounds__(kThreads) k_march(const StepParams<T> p) {
                 km = V{lds[H0][lr][lane], lds[H0][lr + 1][lane]};
                 kp = V{lds[H0][lr][lane + 2], lds[H0][lr + 1][lane + 2]};
             }
-            if constexpr (FAST) {  // --math fma (stencil_math coef_lap_fma)
-                const V l = coef_lap_fma(c, u1[S0][v], u1[S2][v], jm, jp, km, kp, vsplat<L, V>(p.fc[0]),
-                                         vsplat<L, V>(p.fc[1]), vsplat<L, V>(p.fc[2]));
-                vv[v] = FIRST ? c + l : leapfrog_fma(c, u2[H0][v], l);
+            if constexpr (FAST) {  // --math fma (stencil_math coef_lap_fma / leap_fm)
+                const V fx = vsplat<L, V>(p.fc[0]), fy = vsplat<L, V>(p.fc[1]), fz = vsplat<L, V>(p.fc[2]);
+                if constexpr (FIRST)
+                    vv[v] = c + coef_lap_fma(c, u1[S0][v], u1[S2][v], jm, jp, km, kp, fx, fy, fz);
+                else
+                    vv[v] = leap_fm(c, u2[H0][v], u1[S0][v], u1[S2][v], jm, jp, km, kp, fx, fy, fz,
+                                    vsplat<L, V>(fm_kc(p.fc[0], p.fc[1], p.fc[2])));
             } else {
                 const V lap = laplace7_cr(c, u1[S0][v], u1[S2][v], jm, jp, km, kp, hx2, hy2, hz2,
                                           yx2, yy2, yz2);

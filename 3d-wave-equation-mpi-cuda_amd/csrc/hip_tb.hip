@@ -264,28 +264,31 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WP
     T chk1 = T(0), chk2 = T(0);
 
     // layer L (0 = C, 1 = D) arithmetic: exact Laplacian or (FM) coef*Laplacian, and the updates
+    // FM: lap() defers the stencil (FmLap): the leapfrog takes it whole (stencil_math leap_fm),
+    // the Taylor start and the increment form take coef*lap
+    const T kc1 = FM ? fm_kc(p.fc[1][0], p.fc[1][1], p.fc[1][2]) : T(0);
     auto lap = [&](int L, T ctr, T xm, T xp, T ym, T yp, T zm, T zp) {
         if constexpr (FM) {  // fc[0] == fc[1] unless C is the Taylor first layer
             const int f = FIRST && L == 0 ? 0 : 1;
-            return coef_lap_fma(ctr, xm, xp, ym, yp, zm, zp, p.fc[f][0], p.fc[f][1], p.fc[f][2]);
+            return FmLap<T>{ctr, xm, xp, ym, yp, zm, zp, p.fc[f][0], p.fc[f][1], p.fc[f][2]};
         }
         else
             return laplace7_cr(ctr, xm, xp, ym, yp, zm, zp, p.hx2, p.hy2, p.hz2, p.yx2, p.yy2, p.yz2);
     };
-    auto leap = [&](int L, T ctr, T u2, T l) {
-        if constexpr (FM) return leapfrog_fma(ctr, u2, l);
+    auto leap = [&](int L, T ctr, T u2, const auto& l) {
+        if constexpr (FM) return l.leap(u2, kc1);
         else return leapfrog(ctr, u2, l, L == 0 ? p.coefC : p.coefD);
     };
-    auto first1 = [&](T ctr, T l) {
-        if constexpr (FM) return ctr + l;
+    auto first1 = [&](T ctr, const auto& l) {
+        if constexpr (FM) return ctr + lap_value(l);
         else return taylor_first(ctr, l, p.coefC);
     };
-    auto incr = [&](int L, T dprev, T l) {
-        if constexpr (FM) return dprev + l;
+    auto incr = [&](int L, T dprev, const auto& l) {
+        if constexpr (FM) return dprev + lap_value(l);
         else return delta_incr(dprev, l, L == 0 ? p.coefC : p.coefD);
     };
-    auto scaled = [&](T l) {
-        if constexpr (FM) return l;
+    auto scaled = [&](const auto& l) {
+        if constexpr (FM) return lap_value(l);
         else return p.coefC * l;
     };
 
@@ -392,7 +395,7 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WP
 #pragma unroll
         for (int r = 0; r < R; ++r) {
             const int ya = 2 + w * R + r, xa = 2 + kl;
-            const T l = lap(0, a[S1][r], xpA[r], xnA[r], ldsA[H0][ya - 1][xa], ldsA[H0][ya + 1][xa],
+            const auto l = lap(0, a[S1][r], xpA[r], xnA[r], ldsA[H0][ya - 1][xa], ldsA[H0][ya + 1][xa],
                             ldsA[H0][ya][xa - 1], ldsA[H0][ya][xa + 1]);
             T cv;
             if constexpr (DELTA) {
@@ -407,7 +410,7 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WP
         }
         if (ron) {
             const int ya = rj - jt + 2, xa = rk - kb + 2;
-            const T l = lap(0, ra[S1], rxp, rxn, ldsA[H0][ya - 1][xa], ldsA[H0][ya + 1][xa],
+            const auto l = lap(0, ra[S1], rxp, rxn, ldsA[H0][ya - 1][xa], ldsA[H0][ya + 1][xa],
                             ldsA[H0][ya][xa - 1], ldsA[H0][ya][xa + 1]);
             const T cv = FIRST ? first1(ra[S1], l)
                                : (DELTA ? ra[S1] + incr(0, rb[H0], l) : leap(0, ra[S1], rb[H0], l));
@@ -440,7 +443,7 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WP
 #pragma unroll
             for (int r = 0; r < R; ++r) {
                 const int yc = 1 + w * R + r, xc = 1 + kl;
-                const T l = lap(1, c[S3][r], c[S2][r], c[S0][r], ldsC[H1][yc - 1][xc], ldsC[H1][yc + 1][xc],
+                const auto l = lap(1, c[S3][r], c[S2][r], c[S0][r], ldsC[H1][yc - 1][xc], ldsC[H1][yc + 1][xc],
                                 ldsC[H1][yc][xc - 1], ldsC[H1][yc][xc + 1]);
                 if constexpr (DELTA) {
                     dl[H1][r] = incr(1, dl[H1][r], l);  // d^{m+1}

@@ -313,34 +313,36 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WP
     Rel mr3;
     T chk1 = T(0), chk2 = T(0), chk3 = T(0);
 
-    // Layer L (0 = C, 1 = D, 2 = E) arithmetic. lap(): the Laplacian (exact) or coef*Laplacian
-    // (FM); leap / first / incr: the leapfrog, Taylor-start and increment updates from it.
+    // Layer L (0 = C, 1 = D, 2 = E) arithmetic. lap(): the Laplacian (exact) or, FM, the deferred
+    // stencil (FmLap: the leapfrog takes it whole, stencil_math leap_fm; the Taylor start and the
+    // increment form take coef*lap); leap / first / incr: the updates from it.
+    const T kc1 = FM ? fm_kc(p.fc[1][0], p.fc[1][1], p.fc[1][2]) : T(0);
     auto lap = [&](int L, T ctr, T xm, T xp, T ym, T yp, T zm, T zp) {
         if constexpr (FM) {
             const int f = FIRST && L == 0 ? 0 : 1;
-            return coef_lap_fma(ctr, xm, xp, ym, yp, zm, zp, p.fc[f][0], p.fc[f][1], p.fc[f][2]);
+            return FmLap<T>{ctr, xm, xp, ym, yp, zm, zp, p.fc[f][0], p.fc[f][1], p.fc[f][2]};
         } else {
             return laplace7_cr(ctr, xm, xp, ym, yp, zm, zp, p.hx2, p.hy2, p.hz2, p.yx2, p.yy2, p.yz2);
         }
     };
     auto coefL = [&](int L) { return L == 0 ? p.coefC : (L == 1 ? p.coefD : p.coefE); };
-    auto leap = [&](int L, T ctr, T u2, T l) {
-        if constexpr (FM) return leapfrog_fma(ctr, u2, l);
+    auto leap = [&](int L, T ctr, T u2, const auto& l) {
+        if constexpr (FM) return l.leap(u2, kc1);
         else return leapfrog(ctr, u2, l, coefL(L));
     };
-    auto incr = [&](int L, T dprev, T l) {  // increment form: d_new = d_prev + coef*lap
-        if constexpr (FM) return dprev + l;
+    auto incr = [&](int L, T dprev, const auto& l) {  // increment form: d_new = d_prev + coef*lap
+        if constexpr (FM) return dprev + lap_value(l);
         else return delta_incr(dprev, l, coefL(L));
     };
-    auto scaled = [&](int L, T l) {  // coef*lap (FIRST increment: d = coef*lap)
-        if constexpr (FM) return l;
+    auto scaled = [&](int L, const auto& l) {  // coef*lap (FIRST increment: d = coef*lap)
+        if constexpr (FM) return lap_value(l);
         else return coefL(L) * l;
     };
     auto lapA = [&](int H, int y, int x, T ctr, T xm, T xp) {
         return lap(0, ctr, xm, xp, ldsA[H][y - 1][x], ldsA[H][y + 1][x], ldsA[H][y][x - 1], ldsA[H][y][x + 1]);
     };
-    auto cval = [&](T ctr, T bv, T l) {
-        if constexpr (FM) return FIRST ? ctr + l : leapfrog_fma(ctr, bv, l);
+    auto cval = [&](T ctr, T bv, const auto& l) {
+        if constexpr (FM) return FIRST ? ctr + lap_value(l) : l.leap(bv, kc1);
         else return FIRST ? taylor_first(ctr, l, p.coefC) : leapfrog(ctr, bv, l, p.coefC);
     };
     // Errors are taken two planes late: at iteration i those of C(i-2), D(i-2) and E(i-2), all
@@ -503,7 +505,7 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WP
 #pragma unroll
         for (int r = 0; r < R; ++r) {
             const int y = 3 + w * R + r, x = 3 + lane;
-            const T lap = lapA(H0, y, x, a[S1][r], xpA[r], xnA[r]);
+            const auto lap = lapA(H0, y, x, a[S1][r], xpA[r], xnA[r]);
             if constexpr (DELTA) {
                 const T dv = FIRST ? scaled(0, lap) : incr(0, bb[BC][r], lap);
                 dm[H0][r] = cmask(ocd[r], ocm[r], dv);
@@ -516,7 +518,7 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WP
 #pragma unroll
         for (int s = 0; s < RP; ++s) {
             if (W3D_TB3_ABL != 3 && (rg[s] == 1 || rg[s] == 2)) {
-                const T lap = lapA(H0, ry[s], rx[s], ra[s][S1], rxp[s], rxn[s]);
+                const auto lap = lapA(H0, ry[s], rx[s], ra[s][S1], rxp[s], rxn[s]);
                 T cv;
                 if constexpr (DELTA) {
                     const T dv = FIRST ? scaled(0, lap) : incr(0, rb[s][BC], lap);
@@ -550,7 +552,7 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WP
 #pragma unroll
             for (int r = 0; r < R; ++r) {
                 const int y = 2 + w * R + r, x = 2 + lane;  // C tile coordinates
-                const T l = lap(1, c[S3][r], cpx[r], cnx[r], ldsC[H1][y - 1][x], ldsC[H1][y + 1][x],
+                const auto l = lap(1, c[S3][r], cpx[r], cnx[r], ldsC[H1][y - 1][x], ldsC[H1][y + 1][x],
                                 ldsC[H1][y][x - 1], ldsC[H1][y][x + 1]);
                 if constexpr (DELTA) {
                     const T d1 = incr(1, dm[H1][r], l);  // d^{m+1}
@@ -565,7 +567,7 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WP
             for (int s = 0; s < RP; ++s) {
                 if (W3D_TB3_ABL != 3 && rg[s] == 1) {
                     const int y = ry[s] - 1, x = rx[s] - 1;
-                    const T l = lap(1, rc[s][S3], rcp[s], rcn[s], ldsC[H1][y - 1][x], ldsC[H1][y + 1][x],
+                    const auto l = lap(1, rc[s][S3], rcp[s], rcn[s], ldsC[H1][y - 1][x], ldsC[H1][y + 1][x],
                                     ldsC[H1][y][x - 1], ldsC[H1][y][x + 1]);
                     if constexpr (DELTA)
                         ldsD[H0][y - 1][x - 1] = cmask(rcd[s], rcm[s], rc[s][S3] + incr(1, rdm[s][H1], l));
@@ -598,7 +600,7 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WP
 #pragma unroll
             for (int r = 0; r < R; ++r) {
                 const int y = 1 + w * R + r, x = 1 + lane;  // D tile coordinates
-                const T l = lap(2, d[S3][r], d[S2][r], d[S0][r], ldsD[H1][y - 1][x], ldsD[H1][y + 1][x],
+                const auto l = lap(2, d[S3][r], d[S2][r], d[S0][r], ldsD[H1][y - 1][x], ldsD[H1][y + 1][x],
                                 ldsD[H1][y][x - 1], ldsD[H1][y][x + 1]);
                 if constexpr (DELTA) {
                     dm1[H1][r] = incr(2, dm1[H1][r], l);  // d^{m+2}
@@ -736,8 +738,11 @@ __global__ void __launch_bounds__(kThreads) k_seam_c(const SeamCParams<T> p) {
                                      p.fc[0], p.fc[1], p.fc[2]);
             if constexpr (DELTA)
                 v = FIRST ? a + l : a + (o.Bc[c] + l);
-            else
-                v = FIRST ? a + l : leapfrog_fma(a, o.Bc[c], l);
+            else if constexpr (FIRST)
+                v = a + l;
+            else  // the sweeps' leapfrog (stencil_math leap_fm)
+                v = leap_fm(a, o.Bc[c], o.Am[c], o.Ap[c], o.Ac[c - p.sj], o.Ac[c + p.sj], o.Ac[c - 1], o.Ac[c + 1],
+                            p.fc[0], p.fc[1], p.fc[2], fm_kc(p.fc[0], p.fc[1], p.fc[2]));
         } else {
             const T lap = laplace7_cr(a, o.Am[c], o.Ap[c], o.Ac[c - p.sj], o.Ac[c + p.sj], o.Ac[c - 1],
                                       o.Ac[c + 1], p.hx2, p.hy2, p.hz2, p.yx2, p.yy2, p.yz2);

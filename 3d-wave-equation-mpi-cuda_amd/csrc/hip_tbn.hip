@@ -44,6 +44,12 @@
 
 #include "device_common.hpp"
 
+#ifndef W3D_TBN_RINGPRED  // A/B: 0 = ring layers behind per-lane branches
+#define W3D_TBN_RINGPRED 1
+#endif
+#ifndef W3D_TBN_ONE_LDS  // A/B: 1 = all staged tiles in one __shared__ array
+#define W3D_TBN_ONE_LDS 0
+#endif
 #ifndef W3D_TBN_MASKMUL  // A/B: face masks and the fma checksum as products (see cmask)
 #define W3D_TBN_MASKMUL 1
 #endif
@@ -105,7 +111,9 @@ struct TbnGeom {
     // consecutive rows) hit 32 distinct ds_read_b64 bank pairs (an even pitch of 72 doubles put
     // 8 rows on one pair: 4.6x the bank-conflict cycles of k_tb3 in the first tb4 PMC)
     static constexpr int W(int s) { return (kTK + 2 * (D - s)) | 1; }
-    static constexpr int size(int s) { return H(s) * W(s); }
+    static constexpr int cells(int s) { return H(s) * W(s); }
+    static constexpr int size(int s) { return cells(s) + 1; }  // + a trash cell (predicated ring writes)
+    static constexpr int at(int s, int y, int x) { return (y - s) * W(s) + (x - s); }
     static constexpr int off(int s) { return s == 0 ? 0 : off(s - 1) + 2 * size(s - 1); }
     static constexpr int total = off(D);
     // positions of "ring" r: rings 1..D-2 whole, D-1 without corners, D = the 4 corners of ring
@@ -135,12 +143,31 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(1,
     constexpr unsigned ES = sizeof(T);
     constexpr int NU = D - 1;                // own history: U_0 .. U_{D-2}
     constexpr int NRU = D >= 3 ? D - 2 : 1;  // ring history: U_0 .. U_{D-3}
+    // Every staged (layer, buffer) tile is its own __shared__ object: distinct objects cannot
+    // alias, so the compiler may hoist a layer's LDS reads above the previous layer's LDS
+    // writes (other tiles) instead of issuing read -> wait -> compute -> write one layer at a
+    // time (one array with computed offsets serialised them, W3D_TBN_ONE_LDS)
+#if W3D_TBN_ONE_LDS
     __shared__ T lds[Gm::total];
-    // staged layer s, buffer h, A-frame coordinates (y, x)
-    auto L = [&](auto sc, auto hc, int y, int x) -> T& {
+    auto Lo = [&](auto sc, auto hc, int o) -> T& {
         constexpr int s = decltype(sc)::value, h = decltype(hc)::value;
-        return lds[Gm::off(s) + h * Gm::size(s) + (y - s) * Gm::W(s) + (x - s)];
+        return lds[Gm::off(s) + h * Gm::size(s) + o];
     };
+#else
+    constexpr int Z0 = Gm::size(0), Z1 = Gm::size(1), Z2 = Gm::size(D > 2 ? 2 : 1), Z3 = Gm::size(D > 3 ? 3 : 1);
+    __shared__ T t00[Z0], t01[Z0], t10[Z1], t11[Z1], t20[D > 2 ? Z2 : 1], t21[D > 2 ? Z2 : 1],
+        t30[D > 3 ? Z3 : 1], t31[D > 3 ? Z3 : 1];
+    // staged layer s, buffer h, offset o in its frame
+    auto Lo = [&](auto sc, auto hc, int o) -> T& {
+        constexpr int s = decltype(sc)::value, h = decltype(hc)::value;
+        if constexpr (s == 0) return h ? t01[o] : t00[o];
+        else if constexpr (s == 1) return h ? t11[o] : t10[o];
+        else if constexpr (s == 2) return h ? t21[o] : t20[o];
+        else return h ? t31[o] : t30[o];
+    };
+#endif
+    // ... at A-frame coordinates (y, x)
+    auto L = [&](auto sc, auto hc, int y, int x) -> T& { return Lo(sc, hc, Gm::at(decltype(sc)::value, y, x)); };
 
     const int bid = blockIdx.x;
     const int b = find_box(p, bid);
@@ -271,6 +298,22 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(1,
         ra_off[s] = boff(rj, rk, g != 0 && inb(rj, rk));
         rb_off[s] = boff(rj, rk, !FIRST && rcd[s] && inb(rj, rk));
     }
+    // Predicated ring (W3D_TBN_RINGPRED): every lane of a ring slot runs every ring layer its slot
+    // can hold, without a branch, so one plane body is one basic block the scheduler can fill
+    // (the execz branches around ring layers cut it into regions: LDS read -> wait -> compute ->
+    // write, layer by layer). Lanes whose ring does not evaluate layer l read the tile's first own
+    // node and write the trash cell after the tile; staging-only lanes with no ring likewise.
+    int sto[RP], rdo[RP][D - 1], wro[RP][D - 1];
+    sfor<RP>([&](auto sc) {
+        constexpr int s = decltype(sc)::value;
+        sto[s] = rg[s] ? Gm::at(0, ry[s], rx[s]) : Gm::cells(0);
+        sfor<D - 1>([&](auto lc) {
+            constexpr int l = decltype(lc)::value;
+            const bool act = rg[s] >= 1 && rg[s] <= D - 1 - l;
+            rdo[s][l] = act ? Gm::at(l, ry[s], rx[s]) : Gm::at(l, D, D);
+            wro[s][l] = act ? Gm::at(l + 1, ry[s], rx[s]) : Gm::cells(l + 1);
+        });
+    });
 
     // slots (iteration i = i0 + q, phase P = q & 3): A(x) (x - i0 + 1) & 3 -> A(i-1) = P,
     // A(i) = P+1, A(i+1) = P+2, A(i+2) = P+3; B(x) (x - i0) & 1; U_l(x) (x + l - i0) & 3 ->
@@ -337,20 +380,22 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(1,
 
     // layer-l arithmetic: lap() = Laplacian (exact) or coef*Laplacian (FM); upd() = the
     // Taylor start (layer 0 of the first sweep) or the leapfrog from it
+    // FM: lap() defers the stencil (FmLap); the leapfrog takes it whole (stencil_math leap_fm)
+    const T kc1 = FM ? fm_kc(p.fc[1][0], p.fc[1][1], p.fc[1][2]) : T(0);
     auto lap = [&](auto lc, T ctr, T xm, T xp, T ym, T yp, T zm, T zp) {
         constexpr int l = decltype(lc)::value;
         if constexpr (FM) {
             constexpr int f = FIRST && l == 0 ? 0 : 1;
-            return coef_lap_fma(ctr, xm, xp, ym, yp, zm, zp, p.fc[f][0], p.fc[f][1], p.fc[f][2]);
+            return FmLap<T>{ctr, xm, xp, ym, yp, zm, zp, p.fc[f][0], p.fc[f][1], p.fc[f][2]};
         } else {
             return laplace7_cr(ctr, xm, xp, ym, yp, zm, zp, p.hx2, p.hy2, p.hz2, p.yx2, p.yy2, p.yz2);
         }
     };
-    auto upd = [&](auto lc, T ctr, T pw, T l_) {
+    auto upd = [&](auto lc, T ctr, T pw, const auto& l_) {
         constexpr int l = decltype(lc)::value;
         if constexpr (FM) {
-            if constexpr (FIRST && l == 0) return ctr + l_;
-            else return leapfrog_fma(ctr, pw, l_);
+            if constexpr (FIRST && l == 0) return ctr + lap_value(l_);
+            else return l_.leap(pw, kc1);
         } else {
             if constexpr (FIRST && l == 0) return taylor_first(ctr, l_, p.coef[0]);
             else return leapfrog(ctr, pw, l_, p.coef[l]);
@@ -413,7 +458,8 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(1,
         for (int r = 0; r < R; ++r) L(Ic<0>{}, Ic<H0>{}, D + w * R + r, D + lane) = a[S1][r];
 #pragma unroll
         for (int s = 0; s < RP; ++s)
-            if (rg[s]) L(Ic<0>{}, Ic<H0>{}, ry[s], rx[s]) = ra[s][S1];
+            if constexpr (W3D_TBN_RINGPRED) Lo(Ic<0>{}, Ic<H0>{}, sto[s]) = ra[s][S1];
+            else if (rg[s]) L(Ic<0>{}, Ic<H0>{}, ry[s], rx[s]) = ra[s][S1];
         __syncthreads();
 
         T ev[R];  // U_{D-1}(i - D + 1): stored and its errors taken below
@@ -448,7 +494,7 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(1,
                 auto ctr_of = [&](int q) { return l == 0 ? a[S1][q] : u[l > 0 ? l - 1 : 0][S3][q]; };
                 const T ym = r > 0 ? ctr_of(r - 1) : L(lc, Ic<HS>{}, y - 1, xx);
                 const T yp = r < R - 1 ? ctr_of(r + 1) : L(lc, Ic<HS>{}, y + 1, xx);
-                const T lp = lap(lc, ctr, xm, xp, ym, yp, L(lc, Ic<HS>{}, y, xx - 1), L(lc, Ic<HS>{}, y, xx + 1));
+                const auto lp = lap(lc, ctr, xm, xp, ym, yp, L(lc, Ic<HS>{}, y, xx - 1), L(lc, Ic<HS>{}, y, xx + 1));
                 v[r] = cmask(ocd[r], ocm[r], upd(lc, ctr, pw, lp));
                 if constexpr (l <= D - 2) {
                     u[l][S0][r] = v[r];
@@ -460,7 +506,7 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(1,
                 sfor<RP>([&](auto sc) {
                     constexpr int s = decltype(sc)::value;
                     if constexpr (Gm::ring_of(s * NT) <= D - 1 - l) {
-                        if (rg[s] >= 1 && rg[s] <= D - 1 - l) {
+                        if (W3D_TBN_RINGPRED || (rg[s] >= 1 && rg[s] <= D - 1 - l)) {
                             T ctr, xm, xp, pw;
                             auto am1 = [&]() { return ADEEP ? L(Ic<0>{}, Ic<H1>{}, ry[s], rx[s]) : ra[s][S0]; };
                             if constexpr (l == 0) {
@@ -474,12 +520,14 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(1,
                                 if (x == p.an_i) xp = bld<T>(lrs(p.nP[l]), ra_off[s]);
                                 if (x == p.ap_i) xm = bld<T>(lrs(p.pP[l]), ra_off[s]);
                             }
-                            const int y = ry[s], xx = rx[s];
-                            const T lp = lap(lc, ctr, xm, xp, L(lc, Ic<HS>{}, y - 1, xx), L(lc, Ic<HS>{}, y + 1, xx),
-                                             L(lc, Ic<HS>{}, y, xx - 1), L(lc, Ic<HS>{}, y, xx + 1));
+                            const int ro = W3D_TBN_RINGPRED ? rdo[s][l] : Gm::at(l, ry[s], rx[s]);
+                            const int wo = W3D_TBN_RINGPRED ? wro[s][l] : Gm::at(l + 1, ry[s], rx[s]);
+                            constexpr int Wl = Gm::W(l);
+                            const auto lp = lap(lc, ctr, xm, xp, Lo(lc, Ic<HS>{}, ro - Wl), Lo(lc, Ic<HS>{}, ro + Wl),
+                                                Lo(lc, Ic<HS>{}, ro - 1), Lo(lc, Ic<HS>{}, ro + 1));
                             const T cv = cmask(rcd[s], rcm[s], upd(lc, ctr, pw, lp));
                             if constexpr (l <= D - 3) ru[s][l][S0] = cv;
-                            L(Ic<l + 1>{}, Ic<H0>{}, y, xx) = cv;
+                            Lo(Ic<l + 1>{}, Ic<H0>{}, wo) = cv;
                         }
                     }
                 });
