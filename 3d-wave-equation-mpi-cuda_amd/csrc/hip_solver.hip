@@ -1902,10 +1902,12 @@ private:
     // session and replayed with one hipGraphLaunch per solve. Only for runs without host
     // interaction inside the loop (no external transport, checks, checkpoints, profiling,
     // faults); a failed capture falls back to direct launches.
+    // With overlap on, --graph auto launches directly: a replayed capture of the two-stream
+    // overlap ran its branches serialised (8 simulated ranks with modelled 50 GB/s links: 347k
+    // Mpts/s replayed vs 408k launched directly; 2 ranks 348k vs 446k, profiles/overlap_model_r4.txt)
     bool graph_eligible() const {
         return cfg_.graph != 0 && !ext_ && !mirror_ && cfg_.check_every == 0 && cfg_.checkpoint_every == 0 &&
-               cfg_.resume_dir.empty() && fault_.kind.empty() &&
-               true;
+               cfg_.resume_dir.empty() && fault_.kind.empty() && (cfg_.graph == 1 || !overlap_);
     }
 
     void build_graph(RunResult& res) {

@@ -45,6 +45,9 @@
 #ifndef W3D_TB3_MASKMUL  // A/B: fp64 face masks and the fma checksum as products (cmask)
 #define W3D_TB3_MASKMUL 1
 #endif
+#ifndef W3D_TB3_ONE_LDS  // A/B: 1 = the double-buffered tiles as [2] arrays (one object each)
+#define W3D_TB3_ONE_LDS 0
+#endif
 #ifndef W3D_TB3_PAD
 #define W3D_TB3_PAD 0
 #endif
@@ -122,9 +125,23 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WP
     constexpr int NT = NW * 64;
     constexpr int RP = (N1 + N2 + N3 + NT - 1) / NT;  // ring positions per thread
     constexpr unsigned ES = sizeof(T);
+    // one __shared__ object per staged tile and buffer (W3D_TB3_ONE_LDS = 0): distinct objects
+    // cannot alias, so the compiler may move a tile's LDS reads past another tile's writes
+#if W3D_TB3_ONE_LDS
     __shared__ T ldsA[2][AH][AW];
     __shared__ T ldsC[2][CH][CW];
     __shared__ T ldsD[2][DH][DW];
+    auto LA = [&](int h) -> T(*)[AW] { return ldsA[h]; };
+    auto LC = [&](int h) -> T(*)[CW] { return ldsC[h]; };
+    auto LD = [&](int h) -> T(*)[DW] { return ldsD[h]; };
+#else
+    __shared__ T ldsA0[AH][AW], ldsA1[AH][AW];
+    __shared__ T ldsC0[CH][CW], ldsC1[CH][CW];
+    __shared__ T ldsD0[DH][DW], ldsD1[DH][DW];
+    auto LA = [&](int h) -> T(*)[AW] { return h ? ldsA1 : ldsA0; };
+    auto LC = [&](int h) -> T(*)[CW] { return h ? ldsC1 : ldsC0; };
+    auto LD = [&](int h) -> T(*)[DW] { return h ? ldsD1 : ldsD0; };
+#endif
 
     const int bid = blockIdx.x;
     const int b = find_box(p, bid);
@@ -339,7 +356,7 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WP
         else return coefL(L) * l;
     };
     auto lapA = [&](int H, int y, int x, T ctr, T xm, T xp) {
-        return lap(0, ctr, xm, xp, ldsA[H][y - 1][x], ldsA[H][y + 1][x], ldsA[H][y][x - 1], ldsA[H][y][x + 1]);
+        return lap(0, ctr, xm, xp, LA(H)[y - 1][x], LA(H)[y + 1][x], LA(H)[y][x - 1], LA(H)[y][x + 1]);
     };
     auto cval = [&](T ctr, T bv, const auto& l) {
         if constexpr (FM) return FIRST ? ctr + lap_value(l) : l.leap(bv, kc1);
@@ -455,10 +472,10 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WP
         }
         // ---- stage A(i) --------------------------------------------------------------------
 #pragma unroll
-        for (int r = 0; r < R; ++r) ldsA[H0][3 + w * R + r][3 + lane] = a[S1][r];
+        for (int r = 0; r < R; ++r) LA(H0)[3 + w * R + r][3 + lane] = a[S1][r];
 #pragma unroll
         for (int s = 0; s < RP; ++s)
-            if (rg[s]) ldsA[H0][ry[s]][rx[s]] = ra[s][S1];
+            if (rg[s]) LA(H0)[ry[s]][rx[s]] = ra[s][S1];
         __syncthreads();
 
         // ---- seam partners (uniform branch, rare) -------------------------------------------
@@ -513,7 +530,7 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WP
             } else {
                 c[S0][r] = cmask(ocd[r], ocm[r], cval(a[S1][r], bb[BC][r], lap));
             }
-            ldsC[H0][y - 1][x - 1] = c[S0][r];
+            LC(H0)[y - 1][x - 1] = c[S0][r];
         }
 #pragma unroll
         for (int s = 0; s < RP; ++s) {
@@ -528,7 +545,7 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WP
                     cv = cmask(rcd[s], rcm[s], cval(ra[s][S1], rb[s][BC], lap));
                 }
                 rc[s][S0] = cv;
-                ldsC[H0][ry[s] - 1][rx[s] - 1] = cv;
+                LC(H0)[ry[s] - 1][rx[s] - 1] = cv;
             }
         }
         if constexpr (!ALIAS) {
@@ -552,8 +569,8 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WP
 #pragma unroll
             for (int r = 0; r < R; ++r) {
                 const int y = 2 + w * R + r, x = 2 + lane;  // C tile coordinates
-                const auto l = lap(1, c[S3][r], cpx[r], cnx[r], ldsC[H1][y - 1][x], ldsC[H1][y + 1][x],
-                                ldsC[H1][y][x - 1], ldsC[H1][y][x + 1]);
+                const auto l = lap(1, c[S3][r], cpx[r], cnx[r], LC(H1)[y - 1][x], LC(H1)[y + 1][x],
+                                LC(H1)[y][x - 1], LC(H1)[y][x + 1]);
                 if constexpr (DELTA) {
                     const T d1 = incr(1, dm[H1][r], l);  // d^{m+1}
                     dm1[H0][r] = cmask(ocd[r], ocm[r], d1);
@@ -561,18 +578,18 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WP
                 } else {
                     d[S0][r] = cmask(ocd[r], ocm[r], leap(1, c[S3][r], a[S0][r], l));
                 }
-                ldsD[H0][y - 1][x - 1] = d[S0][r];
+                LD(H0)[y - 1][x - 1] = d[S0][r];
             }
 #pragma unroll
             for (int s = 0; s < RP; ++s) {
                 if (W3D_TB3_ABL != 3 && rg[s] == 1) {
                     const int y = ry[s] - 1, x = rx[s] - 1;
-                    const auto l = lap(1, rc[s][S3], rcp[s], rcn[s], ldsC[H1][y - 1][x], ldsC[H1][y + 1][x],
-                                    ldsC[H1][y][x - 1], ldsC[H1][y][x + 1]);
+                    const auto l = lap(1, rc[s][S3], rcp[s], rcn[s], LC(H1)[y - 1][x], LC(H1)[y + 1][x],
+                                    LC(H1)[y][x - 1], LC(H1)[y][x + 1]);
                     if constexpr (DELTA)
-                        ldsD[H0][y - 1][x - 1] = cmask(rcd[s], rcm[s], rc[s][S3] + incr(1, rdm[s][H1], l));
+                        LD(H0)[y - 1][x - 1] = cmask(rcd[s], rcm[s], rc[s][S3] + incr(1, rdm[s][H1], l));
                     else
-                        ldsD[H0][y - 1][x - 1] = cmask(rcd[s], rcm[s], leap(1, rc[s][S3], ra[s][S0], l));
+                        LD(H0)[y - 1][x - 1] = cmask(rcd[s], rcm[s], leap(1, rc[s][S3], ra[s][S0], l));
                 }
             }
             if (FAST || (id >= ib && id <= ie)) {
@@ -600,8 +617,8 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WP
 #pragma unroll
             for (int r = 0; r < R; ++r) {
                 const int y = 1 + w * R + r, x = 1 + lane;  // D tile coordinates
-                const auto l = lap(2, d[S3][r], d[S2][r], d[S0][r], ldsD[H1][y - 1][x], ldsD[H1][y + 1][x],
-                                ldsD[H1][y][x - 1], ldsD[H1][y][x + 1]);
+                const auto l = lap(2, d[S3][r], d[S2][r], d[S0][r], LD(H1)[y - 1][x], LD(H1)[y + 1][x],
+                                LD(H1)[y][x - 1], LD(H1)[y][x + 1]);
                 if constexpr (DELTA) {
                     dm1[H1][r] = incr(2, dm1[H1][r], l);  // d^{m+2}
                     ev[r] = d[S3][r] + dm1[H1][r];

@@ -44,8 +44,11 @@
 
 #include "device_common.hpp"
 
+#ifndef W3D_TBN_GATHER  // LDS reads of a layer ahead of its writes (1), and of the next layer (2)
+#define W3D_TBN_GATHER 1
+#endif
 #ifndef W3D_TBN_RINGPRED  // A/B: 0 = ring layers behind per-lane branches
-#define W3D_TBN_RINGPRED 1
+#define W3D_TBN_RINGPRED 0
 #endif
 #ifndef W3D_TBN_ONE_LDS  // A/B: 1 = all staged tiles in one __shared__ array
 #define W3D_TBN_ONE_LDS 0
@@ -465,9 +468,43 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(1,
         T ev[R];  // U_{D-1}(i - D + 1): stored and its errors taken below
 #pragma unroll
         for (int r = 0; r < R; ++r) ev[r] = T(0);
+        // W3D_TBN_GATHER: the LDS neighbours of a layer (own rows: the outer j neighbour and both
+        // k neighbours; ring slots: all four) are read before any of its writes — one LDS round
+        // trip per layer instead of one per row and ring slot (the compiler cannot move a read
+        // above a possibly aliasing write); 2: the next layer's reads also go ahead of this
+        // layer's arithmetic (they read other tiles than it writes)
+        T gown[2][R][4], gring[2][RP][4];
+        auto gather = [&](auto lc) {
+            constexpr int l = decltype(lc)::value, G = l & 1;
+            constexpr int HS = l == 0 ? H0 : H1;
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                const int y = D + w * R + r, xx = D + lane;
+                if (r == 0) gown[G][r][0] = L(lc, Ic<HS>{}, y - 1, xx);
+                if (r == R - 1) gown[G][r][1] = L(lc, Ic<HS>{}, y + 1, xx);
+                gown[G][r][2] = L(lc, Ic<HS>{}, y, xx - 1);
+                gown[G][r][3] = L(lc, Ic<HS>{}, y, xx + 1);
+            }
+            if constexpr (l <= D - 2)
+                sfor<RP>([&](auto sc) {
+                    constexpr int s = decltype(sc)::value;
+                    if constexpr (Gm::ring_of(s * NT) <= D - 1 - l) {
+                        const int ro = W3D_TBN_RINGPRED ? rdo[s][l] : Gm::at(l, ry[s], rx[s]);
+                        constexpr int Wl = Gm::W(l);
+                        gring[G][s][0] = Lo(lc, Ic<HS>{}, ro - Wl);
+                        gring[G][s][1] = Lo(lc, Ic<HS>{}, ro + Wl);
+                        gring[G][s][2] = Lo(lc, Ic<HS>{}, ro - 1);
+                        gring[G][s][3] = Lo(lc, Ic<HS>{}, ro + 1);
+                    }
+                });
+        };
+        if constexpr (W3D_TBN_GATHER == 2) gather(Ic<0>{});
         sfor<D>([&](auto lc) {
             constexpr int l = decltype(lc)::value;
             constexpr int HS = l == 0 ? H0 : H1;  // buffer of the staged layer read (A: this iteration)
+            constexpr int G = l & 1;
+            if constexpr (W3D_TBN_GATHER == 1) gather(lc);
+            if constexpr (W3D_TBN_GATHER == 2 && l + 1 < D) gather(Ic<l + 1>{});
             const int x = i - l;
             if (!(FAST || (x >= ib - (D - 1 - l) && x <= ie + (D - 1 - l)))) return;
             // ---- own nodes ----
@@ -492,9 +529,17 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(1,
                 // j neighbours inside the wave's R rows come from registers (the same values
                 // as the staged tile), only the outer two from LDS
                 auto ctr_of = [&](int q) { return l == 0 ? a[S1][q] : u[l > 0 ? l - 1 : 0][S3][q]; };
-                const T ym = r > 0 ? ctr_of(r - 1) : L(lc, Ic<HS>{}, y - 1, xx);
-                const T yp = r < R - 1 ? ctr_of(r + 1) : L(lc, Ic<HS>{}, y + 1, xx);
-                const auto lp = lap(lc, ctr, xm, xp, ym, yp, L(lc, Ic<HS>{}, y, xx - 1), L(lc, Ic<HS>{}, y, xx + 1));
+                T ym, yp, zm, zp;
+                if constexpr (W3D_TBN_GATHER) {
+                    ym = r > 0 ? ctr_of(r - 1) : gown[G][r][0];
+                    yp = r < R - 1 ? ctr_of(r + 1) : gown[G][r][1];
+                    zm = gown[G][r][2], zp = gown[G][r][3];
+                } else {
+                    ym = r > 0 ? ctr_of(r - 1) : L(lc, Ic<HS>{}, y - 1, xx);
+                    yp = r < R - 1 ? ctr_of(r + 1) : L(lc, Ic<HS>{}, y + 1, xx);
+                    zm = L(lc, Ic<HS>{}, y, xx - 1), zp = L(lc, Ic<HS>{}, y, xx + 1);
+                }
+                const auto lp = lap(lc, ctr, xm, xp, ym, yp, zm, zp);
                 v[r] = cmask(ocd[r], ocm[r], upd(lc, ctr, pw, lp));
                 if constexpr (l <= D - 2) {
                     u[l][S0][r] = v[r];
@@ -523,8 +568,11 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(1,
                             const int ro = W3D_TBN_RINGPRED ? rdo[s][l] : Gm::at(l, ry[s], rx[s]);
                             const int wo = W3D_TBN_RINGPRED ? wro[s][l] : Gm::at(l + 1, ry[s], rx[s]);
                             constexpr int Wl = Gm::W(l);
-                            const auto lp = lap(lc, ctr, xm, xp, Lo(lc, Ic<HS>{}, ro - Wl), Lo(lc, Ic<HS>{}, ro + Wl),
-                                                Lo(lc, Ic<HS>{}, ro - 1), Lo(lc, Ic<HS>{}, ro + 1));
+                            const auto lp = W3D_TBN_GATHER
+                                                ? lap(lc, ctr, xm, xp, gring[G][s][0], gring[G][s][1], gring[G][s][2],
+                                                      gring[G][s][3])
+                                                : lap(lc, ctr, xm, xp, Lo(lc, Ic<HS>{}, ro - Wl), Lo(lc, Ic<HS>{}, ro + Wl),
+                                                      Lo(lc, Ic<HS>{}, ro - 1), Lo(lc, Ic<HS>{}, ro + 1));
                             const T cv = cmask(rcd[s], rcm[s], upd(lc, ctr, pw, lp));
                             if constexpr (l <= D - 3) ru[s][l][S0] = cv;
                             Lo(Ic<l + 1>{}, Ic<H0>{}, wo) = cv;
