@@ -44,6 +44,9 @@
 
 #include "device_common.hpp"
 
+#ifndef W3D_TBN_ABL  // timing ablations (wrong results): 1 loads, 2 stores, 3 both pinned to one plane
+#define W3D_TBN_ABL 0
+#endif
 #ifndef W3D_TBN_GATHER  // LDS reads of a layer ahead of its writes (1), and of the next layer (2)
 #define W3D_TBN_GATHER 1
 #endif
@@ -442,8 +445,10 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(1,
         // ---- prefetch A(i+ADIST), B(i+BDIST) (own and ring; 0-record descriptors when done) --
         {
             const bool moreA = FAST || i + ADIST <= ie + D, moreB = FAST || i + BDIST <= ie + D - 1;
-            const auto rAn = prs(p.A, i + (moreA ? ADIST : 0), moreA ? pbytes : 0u);
-            const auto rBn = prs(p.B, i + (moreB ? BDIST : 0), moreB ? pbytes : 0u);
+            // timing ablation W3D_TBN_ABL bit 0: the steady loads pinned to plane ib (wrong values)
+            const int ia = (W3D_TBN_ABL & 1) ? ib : i + (moreA ? ADIST : 0), ibn = (W3D_TBN_ABL & 1) ? ib : i + (moreB ? BDIST : 0);
+            const auto rAn = prs(p.A, ia, moreA ? pbytes : 0u);
+            const auto rBn = prs(p.B, ibn, moreB ? pbytes : 0u);
             // ADEEP: A(i-1) of the own nodes is read from LDS below; the ring's too
 #pragma unroll
             for (int r = 0; r < R; ++r) {
@@ -584,7 +589,7 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(1,
             if constexpr (l >= D - 2) {
                 constexpr int o = l - (D - 2);
                 if (FAST || (x >= ib && x <= ie)) {
-                    const auto rd = prs(p.O[o], x, pbytes);
+                    const auto rd = prs(p.O[o], (W3D_TBN_ABL & 2) ? ib : x, pbytes);  // ablation bit 1: stores pinned
 #pragma unroll
                     for (int r = 0; r < R; ++r) bst<2>(v[r], rd, os[r]);
                     if (!FAST && (rare & (1 << o))) {

@@ -308,3 +308,17 @@ def test_fma_math_oracle(C, scheme, dtype):
     else:
         assert fm.max_abs[-1] == pytest.approx(ex.max_abs[-1], rel=2e-2)
     assert _solve(p, ranks=4).max_abs == fm.max_abs
+
+
+def test_fma_leapfrog_keeps_reference_goldens(C):
+    """The fp64 --math fma leapfrog in 9 operations (stencil_math leap_fm: scaled neighbour pairs
+    minus the scaled centre, the leapfrog's 2c - u2 kept), shared by the OpenMP oracle and every
+    HIP kernel, keeps the reference's printed L-inf abs table at N=32 K=20 (6 digits; the max
+    relative error sits at the rounding noise next to f's zero plane)."""
+    import wave3d
+    from wave3d.utils import GOLDEN_N32_K20
+
+    r = _solve(wave3d.WaveProblem(32, timesteps=20, math="fma"))
+    assert r.extra["math"] == "fma"
+    for (a, r_), (ga, gr) in zip(_fmt(r), GOLDEN_N32_K20):
+        assert a == ga and float(r_) == pytest.approx(float(gr), rel=1e-2)

@@ -74,7 +74,9 @@ def test_halo_selftest_can_be_skipped(gpu_prog):
 
 
 MIRROR = [("2,2,2", "tb2", "fp64"), ("1,2,2", "tb2", "fp64"), ("2,2,2", "tb3", "fp64"), ("1,2,2", "tb3", "fp32"),
-          ("2,2,2", "march2", "fp64"), ("1,2,2", "march2", "fp64"), ("2,1,1", "tb3", "fp64")]
+          ("2,2,2", "march2", "fp64"), ("1,2,2", "march2", "fp64"), ("2,1,1", "tb3", "fp64"),
+          # the leapfrog default since round 4: 4-deep halos, seam alias planes of A and B
+          ("2,2,2", "tb4", "fp64"), ("1,2,2", "tb4", "fp32"), ("2,1,1", "tb4", "fp64")]
 
 
 @pytest.mark.parametrize("dims,kernel,dtype", MIRROR)
