@@ -23,9 +23,10 @@ std::string usage() {
            "  --x-self-transport     one x rank: send the periodic wrap through the transport\n"
            "                         to this rank (exercises RCCL send/recv on a single GPU)\n"
            "  --overlap auto|on|off  interior/shell split with the halo on a second stream; auto\n"
-           "                         (default) times the first two solves on / off, keeps the faster\n"
+           "                         (default) times solves 2-5 on / off / on / off, keeps the faster\n"
            "  --no-overlap           = --overlap off\n"
-           "  --kernel K             auto (tb3; fp64 increment form: tb2r2w4) | tb2[r<R>][w<W>] | tb3[r<R>w<W>] | tb4\n"
+           "  --kernel K             auto (leapfrog: tb4; increment form: tb3 fp32 / fma, tb2r2w4 fp64) |\n"
+           "                         tb4 | tb3[r<R>w<W>] | tbn3 | tb2[r<R>][w<W>]\n"
            "                         | march[2|4|8][nt|p|f]\n"
            "                         | naive | flat   (temporal blocking / single-step variants)\n"
            "  --chunk C              i-planes per marching work item\n"

@@ -514,6 +514,7 @@ int tile_order() {
         if (!e || !*e) return 2;
         if (e[0] == 'k') return 0;
         if (e[0] == 'j') return 1;
+        if (e[0] == 'b') return 3;  // XCD blocks (k_tbn; the other sweeps treat it as j-fastest)
         return 2;
     }();
     return order;

@@ -180,7 +180,17 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(1,
     const BoxLaunch Bx = p.box[b];
     int local = bid - Bx.block_begin;
     int tk, tj;
-    if (p.order == 2 && Bx.tiles_j % kXcds == 0) {
+    if (p.order == 3 && Bx.tiles_j % 4 == 0 && Bx.tiles_k % 2 == 0) {
+        // XCD blocks: the 8 XCDs tile the (j, k) tile grid 4 x 2, XCD x running a block of
+        // tiles_j/4 rows x tiles_k/2 k-tiles for every chunk (fewer tile edges between XCDs,
+        // whose halo lines each XCD's L2 fetches separately, than the full-width bands)
+        const int x = local % kXcds, bh = Bx.tiles_j / 4, bw = Bx.tiles_k / 2;
+        local /= kXcds;
+        tj = (x >> 1) * bh + local % bh;
+        local /= bh;
+        tk = (x & 1) * bw + local % bw;
+        local /= bw;
+    } else if (p.order == 2 && Bx.tiles_j % kXcds == 0) {
         // XCD x = id mod 8 runs tile rows [x*hb, x*hb + hb) of every k-tile and chunk
         const int hb = Bx.tiles_j / kXcds, x = local % kXcds;
         local /= kXcds;
