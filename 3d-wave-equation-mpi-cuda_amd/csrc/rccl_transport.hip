@@ -61,7 +61,7 @@ int env_int(const char* k, int dflt) {
 int rccl_max_ctas(const std::string& overlap_mode) {
     const char* e = std::getenv("WAVE3D_RCCL_MAX_CTAS");
     if (e && *e) return std::max(0, std::atoi(e));
-    return overlap_mode == "off" ? 0 : kRcclOverlapMaxCtas;
+    return overlap_mode == "on" ? kRcclOverlapMaxCtas : 0;
 }
 
 // The communicator is non-blocking (config.blocking = 0): initialisation and every enqueue

@@ -19,9 +19,12 @@ std::string rccl_unique_id();  // 128 raw bytes
 
 // CTA budget (ncclConfig_t::maxCTAs) of the halo communicator, fixed when it is created:
 // WAVE3D_RCCL_MAX_CTAS when set (<= 0: RCCL's own budget), else by the run's overlap mode —
-//   off       -> 0: RCCL's own budget. Nothing runs beside the exchange, so a cap could only
-//                slow it (a 2x2x2 rank posts 7 peers' messages in one group).
-//   on, auto  -> kRcclOverlapMaxCtas: the interior sweep runs concurrently on the compute
+//   off, auto -> 0: RCCL's own budget. Nothing runs beside the exchange with overlap off, so a
+//                cap could only slow it (a 2x2x2 rank posts 7 peers' messages in one group);
+//                auto keeps it too: the budget is fixed for the communicator's life, and on 2x2x2
+//                blocks the overlap-off arm is the expected winner of the auto trials (the shell
+//                tax outweighs the hidden exchange, profiles/overlap_model_r4.txt).
+//   on        -> kRcclOverlapMaxCtas: the interior sweep runs concurrently on the compute
 //                stream, and each halo CTA holds a CU the sweep's workgroups then wait for.
 // One MI355X cannot tell the budgets apart (profiles/rccl_ctas_r3.txt: a 1-rank self-send
 // costs the same at 1..8 CTAs and at the default); the JSON records the budget of every run.

@@ -63,7 +63,7 @@ def broadcast_bytes(b: bytes | None, src: int = 0, group=None) -> bytes:
 def rccl_transport(device: int | None = None, group=None, overlap: str = "auto"):
     """Native RCCL transport for this rank; the unique id travels via torch.distributed. The
     communicator's CTA budget follows the run's overlap mode (C.rccl_max_ctas: RCCL's own budget
-    when overlap is off, a cap when the interior sweep runs beside the halo)."""
+    for off and auto, a cap when overlap is forced on and the interior sweep runs beside the halo)."""
     C = load()
     rank, world = dist.get_rank(group), dist.get_world_size(group)
     if device is None:
