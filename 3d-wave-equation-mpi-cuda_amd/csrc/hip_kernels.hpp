@@ -116,6 +116,7 @@ template <class T>
 struct SeamCPlane {
     T* out = nullptr;
     const T *Ac = nullptr, *Am = nullptr, *Ap = nullptr, *Bc = nullptr;
+    T* dout = nullptr;  // increment form: also the new d there (the next stage's Bc)
 };
 // fm: --math fma instantiations (stencil_math coef_lap_fma), not bitwise with the reference.
 // The same operator evaluates any later layer on a partner plane (Ac = layer l-1 there, Am / Ap
@@ -147,11 +148,14 @@ struct TbnSeam {
     const T* pP[kTbnMaxDepth - 1] = {};
 };
 bool tbn_supported(int depth, int rows, int waves, bool fm);
+// the increment form (DELTA): fp32 at depth 4 only
+bool tbn_delta_supported(int depth, int rows, int waves, bool fm, bool fp32);
 template <class T>
 void launch_tbn(int depth, int rows, int waves, bool fm, bool first, const T* A, const T* B, T* O0, T* O1,
                 const GridView& gv, const Box* boxes, int nbox, const Box& cdom, int ei0, int ei1,
                 const Wrap& wrap0, const Wrap& wrap1, const TbnSeam<T>& seam, const T* txy, const T* tz,
-                const T* txr, const T* rtz, const StepCoefs* c, u64* const* err, int chunk, hipStream_t s);
+                const T* txr, const T* rtz, const StepCoefs* c, u64* const* err, int chunk, hipStream_t s,
+                bool delta = false);
 
 // Box halo staging for the temporal-blocking exchange on y/z splits: copy the logical box
 // `b` of a level (origin `grid` = logical (0,0,0), strides of `gv`) to / from a contiguous

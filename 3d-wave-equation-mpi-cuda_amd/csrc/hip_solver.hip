@@ -67,7 +67,8 @@ int comm_cu_reserve() {
 }
 
 constexpr int kMaxLevels = 4;  // time levels: 3 single-step, 4 with two- / three-layer sweeps
-constexpr int kSeamPlanes = 8;  // seam scratch planes: tb3 C at 2 partners; tb4 6 C + 2 D planes
+constexpr int kSeamPlanes = 10;  // seam scratch: tb3 C at 2 partners; tb4 6 C + 2 D planes (+ 2 d planes
+                                 // of the increment form: layer m's d at the partners, stage 2's input)
 
 template <class T>
 struct DevRank {
@@ -163,8 +164,9 @@ public:
         G_ = lay.G;
         L_ = lay.L;
         for (int a = 0; a < 3; ++a) cfg_.dims[a] = lay.dims[a];
-        W3D_REQUIRE(tbd_ < 4 || (!c.delta && tbn_supported(4, tb_rows_, tb_waves_, c.fma)),
-                    "four-layer blocking: leapfrog only, tiles " + std::string(tbn_supported(4, 2, 8, c.fma) ? "r2w8" : "none"));
+        W3D_REQUIRE(tbd_ < 4 || (c.delta ? tbn_delta_supported(4, tb_rows_, tb_waves_, c.fma, c.dtype == DType::F32)
+                                         : tbn_supported(4, tb_rows_, tb_waves_, c.fma)),
+                    "four-layer blocking: tile r2w8; the increment form in fp32 only");
         W3D_REQUIRE(!c.fma || !tb_ || tbd_ == 4 ||
                         (tbd_ == 3 ? (c.delta ? tb3_delta_supported(tb_rows_, tb_waves_, true)
                                               : tb3_supported(tb_rows_, tb_waves_, true))
@@ -184,9 +186,9 @@ public:
             // sweep, lvl(m+1) = u^{m+1}, lvl(m) = d^{m+1}); an odd last layer is one step of
             // the naive/flat kernel reading that d level
             W3D_REQUIRE(tb_ && (tbd_ == 2 ? tb2_delta_supported(tb_rows_, tb_waves_, tb_nwk_) && tb_occ_ == 0
-                                          : tb3_delta_supported(tb_rows_, tb_waves_)),
+                                          : tbd_ == 4 || tb3_delta_supported(tb_rows_, tb_waves_)),
                         "--scheme delta needs a tb2 kernel with an increment-form instantiation (tb2, tb2r2w8, "
-                        "tb2r4w4, tb2r2w8k2) or tb3 / tb3r1w8");
+                        "tb2r4w4, tb2r2w8k2), tb3 / tb3r1w8 or (fp32) tb4");
             kind_ = KernelVariant{};
             kind_.march = false;
             kind_.delta = true;
@@ -1202,40 +1204,46 @@ private:
         const int X = R.topo.X();
         TbnSeam<T> sp;
         auto scratch = [&](int q) { return R.seamc_buf + i64(q) * si + R.plane_off; };
-        auto op = [&](std::vector<SeamCPlane<T>>* v, int q, const T* c, const T* xm, const T* xp, const T* pw) {
+        // increment form: B holds d^{m-1}; the partner planes' layer-m ops also keep their d
+        // (scratch 8 / 9), which stage 2 takes as its Bc in place of the leapfrog's u^{m-1} = A
+        const bool dl = cfg_.delta;
+        auto op = [&](std::vector<SeamCPlane<T>>* v, int q, const T* c, const T* xm, const T* xp, const T* pw,
+                      int dq = -1) {
             W3D_REQUIRE(R.seamc_buf, "seam scratch not allocated");
             SeamCPlane<T> o;
             o.out = scratch(q), o.Ac = c, o.Am = xm, o.Ap = xp, o.Bc = pw;
+            if (dl && dq >= 0) o.dout = scratch(dq);
             if (v) v->push_back(o);
             return scratch(q);
         };
+        auto dpl = [&](int q, const T* leap) { return dl ? static_cast<const T*>(scratch(q)) : leap; };
         auto Ap = [&](int i) { return A + i64(i) * si; };
         auto Bp = [&](int i) { return B + i64(i) * si; };
         const T* aA = R.alias_buf ? R.alias_buf + R.plane_off : nullptr;
         const T* aB = R.alias_bufB ? R.alias_bufB + R.plane_off : nullptr;
         if (R.topo.dims[0] == 1) {
             // next side (ghost 0 = copy of N-1): partner x = N = plane X
-            const T* cX = op(c_ops, 0, Ap(X), Ap(X - 1), Ap(X + 1), Bp(X));
+            const T* cX = op(c_ops, 0, Ap(X), Ap(X - 1), Ap(X + 1), Bp(X), 8);
             const T* cXm = op(c_ops, 1, Ap(X - 1), Ap(X - 2), Ap(X), Bp(X - 1));
             const T* cXp = op(c_ops, 2, Ap(X + 1), Ap(1), Ap(X + 2), Bp(X + 1));  // copy of 1: x- = x=0
-            sp.next_i = 0, sp.nP[0] = Ap(X), sp.nP[1] = cX, sp.nP[2] = op(d_ops, 6, cX, cXm, cXp, Ap(X));
+            sp.next_i = 0, sp.nP[0] = Ap(X), sp.nP[1] = cX, sp.nP[2] = op(d_ops, 6, cX, cXm, cXp, dpl(8, Ap(X)));
             // prev side (ghost X+1 = copy of 1): partner x = 0 = plane 1
-            const T* c1 = op(c_ops, 3, Ap(1), Ap(0), Ap(2), Bp(1));
+            const T* c1 = op(c_ops, 3, Ap(1), Ap(0), Ap(2), Bp(1), 9);
             const T* c0 = op(c_ops, 4, Ap(0), Ap(-1), Ap(X), Bp(0));  // copy of N-1: x+ = x=N
             const T* c2 = op(c_ops, 5, Ap(2), Ap(1), Ap(3), Bp(2));
-            sp.prev_i = X + 1, sp.pP[0] = Ap(1), sp.pP[1] = c1, sp.pP[2] = op(d_ops, 7, c1, c0, c2, Ap(1));
+            sp.prev_i = X + 1, sp.pP[0] = Ap(1), sp.pP[1] = c1, sp.pP[2] = op(d_ops, 7, c1, c0, c2, dpl(9, Ap(1)));
         } else if (R.topo.first(0)) {
             // partner x = N lives on the last x-rank (alias planes); ghost 0 = N-1, plane 2 = global 1
-            const T* cN = op(c_ops, 0, aA, Ap(0), Ap(2), aB);
+            const T* cN = op(c_ops, 0, aA, Ap(0), Ap(2), aB, 8);
             const T* cNm = op(c_ops, 1, Ap(0), Ap(-1), aA, Bp(0));
             const T* c1 = op(c_ops, 2, Ap(2), Ap(1), Ap(3), Bp(2));
-            sp.next_i = 0, sp.nP[0] = aA, sp.nP[1] = cN, sp.nP[2] = op(d_ops, 6, cN, cNm, c1, aA);
+            sp.next_i = 0, sp.nP[0] = aA, sp.nP[1] = cN, sp.nP[2] = op(d_ops, 6, cN, cNm, c1, dpl(8, aA));
         } else if (R.topo.last(0)) {
             // partner x = 0 lives on the first x-rank; plane X-1 = N-1, ghost X+1 = global 1
-            const T* c0 = op(c_ops, 3, aA, Ap(X - 1), Ap(X + 1), aB);
+            const T* c0 = op(c_ops, 3, aA, Ap(X - 1), Ap(X + 1), aB, 9);
             const T* cm = op(c_ops, 4, Ap(X - 1), Ap(X - 2), Ap(X), Bp(X - 1));
             const T* cp = op(c_ops, 5, Ap(X + 1), aA, Ap(X + 2), Bp(X + 1));  // copy of 1: x- = x=0
-            sp.prev_i = X + 1, sp.pP[0] = aA, sp.pP[1] = c0, sp.pP[2] = op(d_ops, 7, c0, cm, cp, aA);
+            sp.prev_i = X + 1, sp.pP[0] = aA, sp.pP[1] = c0, sp.pP[2] = op(d_ops, 7, c0, cm, cp, dpl(9, aA));
         }
         return sp;
     }
@@ -1243,8 +1251,8 @@ private:
     void seam4(DevRank<T>& R, int m, hipStream_t s) {
         std::vector<SeamCPlane<T>> c_ops, d_ops;
         seam_partners4(R, m, &c_ops, &d_ops);
-        launch_seam_c<T>(m == 1, false, cfg_.fma, c_ops.data(), int(c_ops.size()), R.gv, R.cdom, coefs(m), s);
-        launch_seam_c<T>(false, false, cfg_.fma, d_ops.data(), int(d_ops.size()), R.gv, R.cdom, coefs(m + 1), s);
+        launch_seam_c<T>(m == 1, cfg_.delta, cfg_.fma, c_ops.data(), int(c_ops.size()), R.gv, R.cdom, coefs(m), s);
+        launch_seam_c<T>(false, cfg_.delta, cfg_.fma, d_ops.data(), int(d_ops.size()), R.gv, R.cdom, coefs(m + 1), s);
     }
 
     void sweep4(DevRank<T>& R, int m, hipStream_t s, const Box* boxes = nullptr, int nbox = 0) {
@@ -1257,7 +1265,7 @@ private:
         for (int l = 0; l < 4; ++l) c[l] = coefs(m + l), err[l] = R.err + size_t(m + l) * kSlotsPerLayer;
         launch_tbn<T>(4, tb_rows_, tb_waves_, cfg_.fma, m == 1, A, B, R.g[lvl(m + 2)], R.g[lvl(m + 3)], R.gv, boxes,
                       nbox, R.cdom, R.error.i0, R.error.i1, R.wrap3, R.wrap4, sp, R.txy, R.tz, R.rtxy, R.rtz, c,
-                      err, cfg_.chunk, s);
+                      err, cfg_.chunk, s, cfg_.delta);
     }
 
     // the seam pre-kernels of the sweep that starts at layer m (span 3 or 4); `in`: into the

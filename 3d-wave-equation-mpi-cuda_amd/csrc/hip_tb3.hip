@@ -729,6 +729,7 @@ template <class T>
 struct SeamCOp {
     T* out;
     const T *Ac, *Am, *Ap, *Bc;
+    T* dout;  // increment form: d of the evaluated layer too (nullptr: not kept)
 };
 template <class T>
 struct SeamCParams {
@@ -747,14 +748,14 @@ __global__ void __launch_bounds__(kThreads) k_seam_c(const SeamCParams<T> p) {
     const int k = p.kmin + 1 + (int(blockIdx.x) % ktiles) * kTK + int(threadIdx.x & 63);
     if (j > p.jmax - 1 || k > p.kmax - 1) return;
     const i64 c = i64(j) * p.sj + k;
-    T v = T(0);
+    T v = T(0), d = T(0);
     if (j >= p.cj0 && j <= p.cj1 && k >= p.ck0 && k <= p.ck1) {
         const T a = o.Ac[c];
         if constexpr (FM) {  // as the sweep's FM instantiation, so the seam C is the sweep's C
             const T l = coef_lap_fma(a, o.Am[c], o.Ap[c], o.Ac[c - p.sj], o.Ac[c + p.sj], o.Ac[c - 1], o.Ac[c + 1],
                                      p.fc[0], p.fc[1], p.fc[2]);
             if constexpr (DELTA)
-                v = FIRST ? a + l : a + (o.Bc[c] + l);
+                d = FIRST ? l : o.Bc[c] + l, v = a + d;
             else if constexpr (FIRST)
                 v = a + l;
             else  // the sweeps' leapfrog (stencil_math leap_fm)
@@ -764,12 +765,13 @@ __global__ void __launch_bounds__(kThreads) k_seam_c(const SeamCParams<T> p) {
             const T lap = laplace7_cr(a, o.Am[c], o.Ap[c], o.Ac[c - p.sj], o.Ac[c + p.sj], o.Ac[c - 1],
                                       o.Ac[c + 1], p.hx2, p.hy2, p.hz2, p.yx2, p.yy2, p.yz2);
             if constexpr (DELTA)  // Bc = d^{m-1}
-                v = FIRST ? a + p.coef * lap : a + delta_incr(o.Bc[c], lap, p.coef);
+                d = FIRST ? p.coef * lap : delta_incr(o.Bc[c], lap, p.coef), v = a + d;
             else
                 v = FIRST ? taylor_first(a, lap, p.coef) : leapfrog(a, o.Bc[c], lap, p.coef);
         }
     }
     o.out[c] = v;
+    if (DELTA && o.dout) o.dout[c] = d;
 }
 
 template <class T, bool F>
@@ -915,7 +917,7 @@ void launch_seam_c(bool first, bool delta, bool fm, const SeamCPlane<T>* ops, in
     if (nops == 0) return;
     SeamCParams<T> p{};
     for (int q = 0; q < nops; ++q)
-        p.op[q] = SeamCOp<T>{ops[q].out, ops[q].Ac, ops[q].Am, ops[q].Ap, ops[q].Bc ? ops[q].Bc : ops[q].Ac};
+        p.op[q] = SeamCOp<T>{ops[q].out, ops[q].Ac, ops[q].Am, ops[q].Ap, ops[q].Bc ? ops[q].Bc : ops[q].Ac, ops[q].dout};
     p.sj = gv.sj;
     p.jmin = 1 - gv.G, p.jmax = gv.jmax(), p.kmin = 1 - gv.G, p.kmax = gv.kmax();
     p.cj0 = cdom.j0, p.cj1 = cdom.j1, p.ck0 = cdom.k0, p.ck1 = cdom.k1;

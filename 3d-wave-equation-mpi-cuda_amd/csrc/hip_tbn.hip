@@ -137,7 +137,11 @@ struct TbnGeom {
     }
 };
 
-template <class T, int D, bool FIRST, int R, int NW, bool FM, int DEEP>
+// DELTA: the increment form (as k_tb3's): B = d^{m-1}; layer l keeps d_l = d_{l-1} + coef lap U_{l-1}
+// (d_{-1} = B, U_{-1} = A) and U_l = U_{l-1} + d_l; d is pointwise, so it rides in registers from
+// one layer to the next (same plane, next iteration) and never in LDS. The sweep stores d and U of
+// its last layer (O[0] = the next sweep's B, O[1] its A), with the last layer's self-wrap ranges.
+template <class T, int D, bool FIRST, int R, int NW, bool FM, int DEEP, bool DELTA = false>
 __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(1, 8))) k_tbn(const TbnParams<T> p) {
     constexpr bool ADEEP = DEEP & 1;      // A(i+3) into the slot of A(i-1) (read from LDS)
     constexpr int NB = DEEP & 2 ? 4 : 2;  // B slots: B(i + NB/2) prefetched at iteration i
@@ -271,7 +275,8 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(1,
     cut(p.ap_i, p.ap_i + D - 2);
 #pragma unroll
     for (int g = 0; g < 2; ++g) {
-        cut(p.w_lo[0][g] + D - 2, p.w_hi[0][g] + D - 2);
+        // O[0]'s stores run at iteration x + D - 2 (leapfrog: U_{D-2}) or x + D - 1 (DELTA: d_{D-1})
+        cut(p.w_lo[0][g] + (DELTA ? D - 1 : D - 2), p.w_hi[0][g] + (DELTA ? D - 1 : D - 2));
         cut(p.w_lo[1][g] + D - 1, p.w_hi[1][g] + D - 1);
     }
     flo = __builtin_amdgcn_readfirstlane(flo);
@@ -388,6 +393,19 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(1,
         if constexpr (W3D_TBN_MASKMUL) return v * m;
         else return keep ? v : T(0);
     };
+    // increment form: d_l of the own rows / ring slots in a plane-parity slot (written at
+    // iteration i for plane i - l, read by layer l+1 at iteration i+1: the same plane)
+    constexpr int ND = DELTA ? D - 1 : 1, NRD = DELTA && D >= 3 ? D - 2 : 1;
+    T dq[ND][2][R], rdq[RP][NRD][2];
+#pragma unroll
+    for (int l = 0; l < ND; ++l)
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+#pragma unroll
+            for (int r = 0; r < R; ++r) dq[l][h][r] = T(0);
+#pragma unroll
+            for (int s = 0; s < RP; ++s) rdq[s][l < NRD ? l : 0][h] = T(0);
+        }
     using Rel = std::conditional_t<FM, RelMax<T>, RelArg<T>>;  // fma: |d| * 1/|f| max
     T ma[D], chk[D];
     Rel mr[D];
@@ -405,6 +423,17 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(1,
             return FmLap<T>{ctr, xm, xp, ym, yp, zm, zp, p.fc[f][0], p.fc[f][1], p.fc[f][2]};
         } else {
             return laplace7_cr(ctr, xm, xp, ym, yp, zm, zp, p.hx2, p.hy2, p.hz2, p.yx2, p.yy2, p.yz2);
+        }
+    };
+    // increment form: d_l from d_{l-1} (FIRST layer 0: coef*lap alone)
+    auto dnew = [&](auto lc, T dprev, const auto& l_) {
+        constexpr int l = decltype(lc)::value;
+        if constexpr (FM) {
+            if constexpr (FIRST && l == 0) return lap_value(l_);
+            else return dprev + lap_value(l_);
+        } else {
+            if constexpr (FIRST && l == 0) return p.coef[0] * l_;
+            else return delta_incr(dprev, l_, p.coef[l]);
         }
     };
     auto upd = [&](auto lc, T ctr, T pw, const auto& l_) {
@@ -523,7 +552,7 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(1,
             const int x = i - l;
             if (!(FAST || (x >= ib - (D - 1 - l) && x <= ie + (D - 1 - l)))) return;
             // ---- own nodes ----
-            T v[R];
+            T v[R], dl[R];  // dl: the increment form's d of the last layer (stored to O[0])
 #pragma unroll
             for (int r = 0; r < R; ++r) {
                 const int y = D + w * R + r, xx = D + lane;
@@ -555,7 +584,15 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(1,
                     zm = L(lc, Ic<HS>{}, y, xx - 1), zp = L(lc, Ic<HS>{}, y, xx + 1);
                 }
                 const auto lp = lap(lc, ctr, xm, xp, ym, yp, zm, zp);
-                v[r] = cmask(ocd[r], ocm[r], upd(lc, ctr, pw, lp));
+                if constexpr (DELTA) {
+                    const T dprev = l == 0 ? bb[BC][r] : dq[l > 0 ? l - 1 : 0][H1][r];
+                    const T dv = cmask(ocd[r], ocm[r], dnew(lc, dprev, lp));
+                    v[r] = cmask(ocd[r], ocm[r], ctr + dv);
+                    if constexpr (l <= D - 2) dq[l][H0][r] = dv;
+                    else dl[r] = dv;
+                } else {
+                    v[r] = cmask(ocd[r], ocm[r], upd(lc, ctr, pw, lp));
+                }
                 if constexpr (l <= D - 2) {
                     u[l][S0][r] = v[r];
                     L(Ic<l + 1>{}, Ic<H0>{}, y, xx) = v[r];
@@ -588,29 +625,41 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(1,
                                                       gring[G][s][3])
                                                 : lap(lc, ctr, xm, xp, Lo(lc, Ic<HS>{}, ro - Wl), Lo(lc, Ic<HS>{}, ro + Wl),
                                                       Lo(lc, Ic<HS>{}, ro - 1), Lo(lc, Ic<HS>{}, ro + 1));
-                            const T cv = cmask(rcd[s], rcm[s], upd(lc, ctr, pw, lp));
+                            T cv;
+                            if constexpr (DELTA) {
+                                const T dprev = l == 0 ? rb[s][BC] : rdq[s][l > 0 ? l - 1 : 0][H1];
+                                const T dv = cmask(rcd[s], rcm[s], dnew(lc, dprev, lp));
+                                cv = cmask(rcd[s], rcm[s], ctr + dv);
+                                if constexpr (l <= D - 3) rdq[s][l][H0] = dv;
+                            } else {
+                                cv = cmask(rcd[s], rcm[s], upd(lc, ctr, pw, lp));
+                            }
                             if constexpr (l <= D - 3) ru[s][l][S0] = cv;
                             Lo(Ic<l + 1>{}, Ic<H0>{}, wo) = cv;
                         }
                     }
                 });
             }
-            // ---- stores of the last two layers (own planes, + periodic self-wrap) ----
-            if constexpr (l >= D - 2) {
-                constexpr int o = l - (D - 2);
+            // ---- stores of the last two layers (own planes, + periodic self-wrap); the increment
+            // form stores d and U of the last layer (O[0] then has the last layer's wrap ranges) --
+            auto put = [&](const int o, const T(&val)[R]) {
+                const auto rd = prs(p.O[o], (W3D_TBN_ABL & 2) ? ib : x, pbytes);  // ablation bit 1: stores pinned
+#pragma unroll
+                for (int r = 0; r < R; ++r) bst<2>(val[r], rd, os[r]);
+                if (!FAST && (rare & (1 << o))) {
+#pragma unroll
+                    for (int g = 0; g < 2; ++g)
+                        if (x >= p.w_lo[o][g] && x <= p.w_hi[o][g]) {
+                            const auto rw = prs(p.O[o], x + p.w_sh[o][g], pbytes);
+#pragma unroll
+                            for (int r = 0; r < R; ++r) bst<2>(val[r], rw, os[r]);
+                        }
+                }
+            };
+            if constexpr (DELTA ? l == D - 1 : l >= D - 2) {
                 if (FAST || (x >= ib && x <= ie)) {
-                    const auto rd = prs(p.O[o], (W3D_TBN_ABL & 2) ? ib : x, pbytes);  // ablation bit 1: stores pinned
-#pragma unroll
-                    for (int r = 0; r < R; ++r) bst<2>(v[r], rd, os[r]);
-                    if (!FAST && (rare & (1 << o))) {
-#pragma unroll
-                        for (int g = 0; g < 2; ++g)
-                            if (x >= p.w_lo[o][g] && x <= p.w_hi[o][g]) {
-                                const auto rw = prs(p.O[o], x + p.w_sh[o][g], pbytes);
-#pragma unroll
-                                for (int r = 0; r < R; ++r) bst<2>(v[r], rw, os[r]);
-                            }
-                    }
+                    if constexpr (DELTA) put(0, dl);
+                    put(DELTA ? 1 : l - (D - 2), v);
                 }
             }
             if constexpr (l == D - 1) {
@@ -729,7 +778,15 @@ int tbn_deep() {
 }
 
 template <class T, int D, bool F>
-static void (*tbn_kernel(int rows, int waves, bool fm, int deep))(const TbnParams<T>) {
+static void (*tbn_kernel(int rows, int waves, bool fm, int deep, bool delta))(const TbnParams<T>) {
+    // the increment form: fp32 at depth 4 (config 5's scheme; the fp64 one needs ~30 more VGPRs
+    // than the 248 of the leapfrog sweep has room for)
+    if (delta) {
+        if constexpr (std::is_same_v<T, float> && D == 4)
+            if (deep == kTbnDeep && rows == 2 && waves == 8)
+                return fm ? k_tbn<T, D, F, 2, 8, true, kTbnDeep, true> : k_tbn<T, D, F, 2, 8, false, kTbnDeep, true>;
+        return nullptr;
+    }
 #ifdef W3D_TBN_ONLY  // codegen experiments: one instantiation (fp64, fma, not first, default DEEP)
 #ifndef W3D_TBN_PROBE_R
 #define W3D_TBN_PROBE_R 2
@@ -757,10 +814,10 @@ static void (*tbn_kernel(int rows, int waves, bool fm, int deep))(const TbnParam
 }
 
 template <class T, bool F>
-static void (*tbn_kernel_d(int depth, int rows, int waves, bool fm, int deep))(const TbnParams<T>) {
-    if (depth == 4) return tbn_kernel<T, 4, F>(rows, waves, fm, deep);
+static void (*tbn_kernel_d(int depth, int rows, int waves, bool fm, int deep, bool delta = false))(const TbnParams<T>) {
+    if (depth == 4) return tbn_kernel<T, 4, F>(rows, waves, fm, deep, delta);
     if constexpr (std::is_same_v<T, double>)  // depth 3: fp64 (the cross-check of k_tb3, A/B)
-        if (depth == 3) return tbn_kernel<T, 3, F>(rows, waves, fm, deep);
+        if (depth == 3) return tbn_kernel<T, 3, F>(rows, waves, fm, deep, delta);
     return nullptr;
 }
 
@@ -769,21 +826,26 @@ static void (*tbn_kernel_d(int depth, int rows, int waves, bool fm, int deep))(c
 bool tbn_supported(int depth, int rows, int waves, bool fm) {
     return tbn_kernel_d<double, false>(depth, rows, waves, fm, kTbnDeep) != nullptr;
 }
+bool tbn_delta_supported(int depth, int rows, int waves, bool fm, bool fp32) {
+    return fp32 ? tbn_kernel_d<float, false>(depth, rows, waves, fm, kTbnDeep, true) != nullptr
+                : tbn_kernel_d<double, false>(depth, rows, waves, fm, kTbnDeep, true) != nullptr;
+}
 
 template <class T>
 void launch_tbn(int depth, int rows, int waves, bool fm, bool first, const T* A, const T* B, T* O0, T* O1,
                 const GridView& gv, const Box* boxes, int nbox, const Box& cdom, int ei0, int ei1,
                 const Wrap& wrap0, const Wrap& wrap1, const TbnSeam<T>& seam, const T* txy, const T* tz,
-                const T* txr, const T* rtz, const StepCoefs* c, u64* const* err, int chunk, hipStream_t s) {
+                const T* txr, const T* rtz, const StepCoefs* c, u64* const* err, int chunk, hipStream_t s,
+                bool delta) {
     W3D_REQUIRE(depth >= 3 && depth <= kTbnMaxDepth, "tbn: depth 3..4");
     W3D_REQUIRE(!fm || (txr && rtz), "tbn --math fma needs the reciprocal analytic tables");
     W3D_REQUIRE(gv.G >= depth, "deep temporal blocking needs ghost depth >= layers per sweep");
     W3D_REQUIRE(nbox >= 1 && nbox <= kMaxBoxes, "bad box count");
     W3D_REQUIRE(gv.si * i64(sizeof(T)) < (i64(1) << 31), "tbn: plane larger than 2 GiB");
     const int deep = tbn_deep();
-    auto kern = first ? tbn_kernel_d<T, true>(depth, rows, waves, fm, deep)
-                      : tbn_kernel_d<T, false>(depth, rows, waves, fm, deep);
-    W3D_REQUIRE(kern, "tbn: no instantiation of this depth x tile x dtype x math x WAVE3D_TBN_DEEP");
+    auto kern = first ? tbn_kernel_d<T, true>(depth, rows, waves, fm, deep, delta)
+                      : tbn_kernel_d<T, false>(depth, rows, waves, fm, deep, delta);
+    W3D_REQUIRE(kern, "tbn: no instantiation of this depth x tile x dtype x math x scheme x WAVE3D_TBN_DEEP");
     TbnParams<T> p{};
     p.pbytes = unsigned(gv.si * i64(sizeof(T)));
     p.pbias = gv.G + 1;  // plane indices reach ib - depth >= 1 - G and the wrap targets
@@ -866,7 +928,7 @@ void launch_tbn(int depth, int rows, int waves, bool fm, bool first, const T* A,
     template void launch_tbn<T>(int, int, int, bool, bool, const T*, const T*, T*, T*, const GridView&,         \
                                 const Box*, int, const Box&, int, int, const Wrap&, const Wrap&,                \
                                 const TbnSeam<T>&, const T*, const T*, const T*, const T*, const StepCoefs*,   \
-                                u64* const*, int, hipStream_t);
+                                u64* const*, int, hipStream_t, bool);
 W3D_TBN_INST(double)
 W3D_TBN_INST(float)
 

@@ -553,3 +553,55 @@ def test_tb4_overlap_concurrent_interior_bitwise(C, dims, K):
     assert r.extra["overlap"] is True and r.extra["overlap_interior"] > 0
     ref = _solve(p, backend="cpu", threads=8)
     assert r.max_abs == ref.max_abs and r.max_rel == ref.max_rel
+
+
+@pytest.mark.parametrize("math", ["exact", "fma"])
+@pytest.mark.parametrize("ranks,dims,overlap", [(0, None, True), (2, [2, 1, 1], True), (8, [2, 2, 2], True),
+                                                (4, [1, 2, 2], False), (3, [3, 1, 1], False)])
+def test_tb4_delta_fp32_matches_cpu(C, math, ranks, dims, overlap):
+    """The fp32 increment form on four-layer sweeps (k_tbn DELTA: d rides in registers from layer
+    to layer, the sweep stores d and u of its last layer; the seam stages keep layer m's d at the
+    partner planes for stage 2) == the OpenMP oracle's increment form bit for bit, K = 10..13
+    (tb3 / tb2 / single-step tails), one rank, x slabs and 3-D blocks, with and without overlap
+    (--math fma: the values and max abs errors bit for bit, the relative error within ulps)."""
+    import wave3d
+
+    for K in (10, 11, 12, 13):
+        p = wave3d.WaveProblem(29, Lx=1.3, Ly="pi", Lz=2.0, timesteps=K, ic="shifted", dtype="fp32",
+                               scheme="delta", math=math)
+        ref = _solve(p, backend="cpu", threads=4)
+        got = _solve(p, kernel="tb4", ranks=ranks, dims=dims, overlap=overlap)
+        assert got.kernel == "tb4" and got.extra["scheme"] == "delta"
+        assert got.max_abs == ref.max_abs
+        if math == "exact":
+            assert got.max_rel == ref.max_rel
+        else:  # --math fma: the relative error from reciprocal tables, within ulps (RelMax)
+            assert got.max_rel == pytest.approx(ref.max_rel, rel=1e-5)
+
+
+def test_tb4_delta_fp32_resume_and_accuracy(C, tmp_path):
+    """Checkpoint / resume of the fp32 increment form across four-layer sweeps (the d level is the
+    sweep's first stored slot), bitwise with the uninterrupted run; the N=128 K=400 accuracy of
+    the increment form (at the fp64 error, where fp32 leapfrog is far off) holds on tb4."""
+    import wave3d
+
+    p = wave3d.WaveProblem(40, timesteps=17, ic="shifted", dtype="fp32", scheme="delta")
+    full = _solve(p, kernel="tb4", ranks=2)
+    _solve(p, kernel="tb4", ranks=2, checkpoint_every=6, checkpoint_dir=str(tmp_path))
+    res = _solve(p, kernel="tb4", ranks=2, resume=str(tmp_path))
+    assert res.extra["resumed_from"] == 12
+    assert res.max_abs == full.max_abs and res.max_rel == full.max_rel
+    e64 = _solve(wave3d.WaveProblem(128, timesteps=400)).linf_abs
+    d = _solve(wave3d.WaveProblem(128, timesteps=400, dtype="fp32", scheme="delta"), kernel="tb4").linf_abs
+    assert d < 1.2 * e64
+
+
+def test_tb4_delta_fp64_is_refused(C):
+    """The fp64 increment form has no four-layer instantiation (register budget): asking for it
+    fails with a message, the auto kernel keeps tb3 / tb2 there."""
+    import wave3d
+
+    p = wave3d.WaveProblem(24, timesteps=8, scheme="delta")
+    with pytest.raises(Exception, match="increment form"):
+        _solve(p, kernel="tb4")
+    assert _solve(p).kernel != "tb4"
