@@ -61,6 +61,12 @@ std::string tb_name(int rows, int waves, int occ, int depth = 2, int kwaves = 1)
 // CUs the compute stream leaves to the halo stream while overlap is on (WAVE3D_COMM_CUS,
 // default kCommCus; 0 = no CU-masked stream)
 constexpr int kCommCus = 0;
+// Overlap order of the deep sweeps (WAVE3D_OVERLAP_SHELLS_FIRST=1): the shells first on the compute
+// stream, then the exchange beside the interior; default: the shells beside the interior
+bool overlap_shells_first() {
+    const char* e = std::getenv("WAVE3D_OVERLAP_SHELLS_FIRST");
+    return e && e[0] == '1';
+}
 int comm_cu_reserve() {
     const char* e = std::getenv("WAVE3D_COMM_CUS");
     return e && *e ? std::max(0, std::atoi(e)) : kCommCus;
@@ -1813,7 +1819,29 @@ private:
                 for (auto& R : ranks_)
                     if ((first_write_[q + 1] || q == start) && !(span >= 3 && q < n + span - 2))
                         launch_zero_faces<T>(R.g[lvl(q)], R.gv, R.zero_mask, s_comp_);
-            if (span >= 3 && overlap_) {
+            bool exchanged = false;  // the exchange of this sweep's last layer is already enqueued
+            if (span >= 3 && overlap_ && shells_first_) {
+                // Shells first (WAVE3D_OVERLAP_SHELLS_FIRST): after the previous halo, the shells run
+                // on the compute stream as one launch over the whole GPU (work items sized for it),
+                // then the next exchange starts on the comm stream while the interior sweeps. The
+                // shells no longer share the GPU with the interior for the whole sweep, which a
+                // full-length tile band in j or k otherwise does (the z shell is a 64-column band).
+                HIP_CHECK(hipStreamWaitEvent(s_comp_, ev_halo_, 0));
+                for (auto& R : ranks_) {
+                    seam_pre(R, n, span, s_comp_);
+                    if (!R.tb_shell.empty())
+                        sweep_deep(R, n, span, s_comp_, R.tb_shell.data(), int(R.tb_shell.size()));
+                }
+                const int last = n + span - 1;
+                if (last < K) {
+                    HIP_CHECK(hipEventRecord(ev_shell_, s_comp_));
+                    HIP_CHECK(hipStreamWaitEvent(s_comm_, ev_shell_, 0));
+                    issue_exchange(last, true);
+                    exchanged = true;
+                }
+                for (auto& R : ranks_)
+                    if (!R.tb_interior.empty()) sweep_deep(R, n, span, s_comp_, &R.tb_interior, 1);
+            } else if (span >= 3 && overlap_) {
                 // Shells on the (high-priority) comm stream right behind the previous halo,
                 // concurrently with the interior on the compute stream, as the two-layer path:
                 // the shells need that halo and the previous sweep's interior; the interior reads
@@ -1889,7 +1917,7 @@ private:
                 for (auto& R : ranks_) inject_after_compute(R, q, s_comp_, q == first_stored ? n : q);
             mark(s_comp_, 1);
             const int last = n + span - 1;
-            if (last < K) issue_exchange(last, comm_follows);
+            if (last < K && !exchanged) issue_exchange(last, comm_follows);
             done = last;
             bool ck = false, stop = false;
             for (int q = n; q <= last; ++q) {
@@ -2204,6 +2232,7 @@ private:
     std::vector<char> first_write_;  // layer n is the first write of its buffer in the solve
     bool overlap_ = false;
     bool overlap_auto_ = false;   // --overlap auto with a remote halo
+    bool shells_first_ = overlap_shells_first();  // deep sweeps: shells, then exchange || interior
     static constexpr int kOverlapTrials = 4;  // overlap auto trial solves: on, off, on, off
     int trials_done_ = 0;         // overlap auto trials run
     int solves_ = 0;              // solves of this session
