@@ -44,19 +44,20 @@
 
 #include "device_common.hpp"
 
+// Build-time A/B switches, measured in profiles/deep_sweeps_r4.txt (the defaults are the winners):
 #ifndef W3D_TBN_ABL  // timing ablations (wrong results): 1 loads, 2 stores, 3 both pinned to one plane
 #define W3D_TBN_ABL 0
 #endif
-#ifndef W3D_TBN_GATHER  // LDS reads of a layer ahead of its writes (1), and of the next layer (2)
-#define W3D_TBN_GATHER 1
+#ifndef W3D_TBN_GATHER  // a layer's LDS reads ahead of its writes (1: +0.6 % fma, +1.3 % exact), and
+#define W3D_TBN_GATHER 1  // also the next layer's (2: spills at 256 VGPRs, -11 %)
 #endif
-#ifndef W3D_TBN_RINGPRED  // A/B: 0 = ring layers behind per-lane branches
+#ifndef W3D_TBN_RINGPRED  // 1: ring layers without branches (one basic block per plane), -1.6 %
 #define W3D_TBN_RINGPRED 0
 #endif
-#ifndef W3D_TBN_ONE_LDS  // A/B: 1 = all staged tiles in one __shared__ array
+#ifndef W3D_TBN_ONE_LDS  // 1: all staged tiles in one __shared__ array (-1 %)
 #define W3D_TBN_ONE_LDS 0
 #endif
-#ifndef W3D_TBN_MASKMUL  // A/B: face masks and the fma checksum as products (see cmask)
+#ifndef W3D_TBN_MASKMUL  // face masks and the fma checksum as products (see cmask; 0: selects, -3 %)
 #define W3D_TBN_MASKMUL 1
 #endif
 
@@ -319,11 +320,10 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(1,
         ra_off[s] = boff(rj, rk, g != 0 && inb(rj, rk));
         rb_off[s] = boff(rj, rk, !FIRST && rcd[s] && inb(rj, rk));
     }
-    // Predicated ring (W3D_TBN_RINGPRED): every lane of a ring slot runs every ring layer its slot
-    // can hold, without a branch, so one plane body is one basic block the scheduler can fill
-    // (the execz branches around ring layers cut it into regions: LDS read -> wait -> compute ->
-    // write, layer by layer). Lanes whose ring does not evaluate layer l read the tile's first own
-    // node and write the trash cell after the tile; staging-only lanes with no ring likewise.
+    // Predicated ring (W3D_TBN_RINGPRED=1, off: measured 1.6 % slower): every lane of a ring slot
+    // runs every ring layer its slot can hold, without a branch, so one plane body is one basic
+    // block; lanes whose ring does not evaluate layer l read the tile's first own node and write
+    // the trash cell after the tile, staging-only lanes with no ring likewise.
     int sto[RP], rdo[RP][D - 1], wro[RP][D - 1];
     sfor<RP>([&](auto sc) {
         constexpr int s = decltype(sc)::value;

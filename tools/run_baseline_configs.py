@@ -34,6 +34,7 @@ def main():
                     help="run multi-GPU configs that do not fit as simulated ranks on ONE GPU "
                          "(loopback halos, subdomains serialised: checks accuracy and "
                          "decomposition cost, NOT a scaling number; rows are marked 'sim')")
+    ap.add_argument("--math", default="exact", choices=["exact", "fma"], help="the GPU configs' arithmetic")
     a = ap.parse_args()
 
     import wave3d
@@ -51,6 +52,8 @@ def main():
         if a.only and name not in a.only:
             continue
         p, be, Np, dims = cfg["problem"], cfg["backend"], cfg["Np"], cfg["dims"]
+        if be == "hip":
+            p.math = a.math
         golden = presets.GOLDEN_LINF.get((p.N, p.timesteps))
         sim = be == "hip" and Np > ngpu and a.simulate and ngpu >= 1
         if be == "hip" and Np > ngpu and not sim:
