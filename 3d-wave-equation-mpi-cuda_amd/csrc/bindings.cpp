@@ -291,7 +291,7 @@ void k_tbn_dense(int depth, int rows, int waves, bool fm, bool first, uintptr_t 
                  uintptr_t O1, const std::vector<i64>& g, const std::vector<std::vector<int>>& boxes,
                  const std::vector<int>& cdom, int ei0, int ei1, uintptr_t tx, uintptr_t ty, uintptr_t tz,
                  const std::vector<std::vector<double>>& coefs, const std::vector<uintptr_t>& err, int chunk,
-                 uintptr_t stream) {
+                 uintptr_t stream, bool delta) {
     i64 o = 0;
     const GridView v = gview_g(g, o);
     W3D_REQUIRE(int(coefs.size()) == depth && int(err.size()) == depth, "k_tbn: one coefficient set / slot per layer");
@@ -317,7 +317,7 @@ void k_tbn_dense(int depth, int rows, int waves, bool fm, bool first, uintptr_t 
         }
         launch_tbn<T>(depth, rows, waves, fm, first, P<T>(A) + o, P<T>(B) + o, P<T>(O0) + o, P<T>(O1) + o, v,
                       bx.data(), int(bx.size()), tobox(cdom), ei0, ei1, Wrap{}, Wrap{}, TbnSeam<T>{}, txy, P<T>(tz),
-                      rt, fm ? rt + 2 * ntxy : nullptr, cs, es, chunk, s);
+                      rt, fm ? rt + 2 * ntxy : nullptr, cs, es, chunk, s, delta);
     } catch (...) {
         (void)hipStreamSynchronize(s);
         (void)hipFree(txy);
@@ -553,6 +553,7 @@ PYBIND11_MODULE(_wave3d_C, m) {
     m.def("k_tbn_f64", &k_tbn_dense<double>);
     m.def("k_tbn_f32", &k_tbn_dense<float>);
     m.def("tbn_supported", &tbn_supported);
+    m.def("tbn_delta_supported", &tbn_delta_supported);
     m.def("tb_supported", [](int depth, int rows, int waves, int nwk, bool fm) {
         return depth == 3 ? tb3_supported(rows, waves, fm) : tb2_supported(rows, waves, 0, nwk);
     }, py::arg("depth"), py::arg("rows"), py::arg("waves"), py::arg("nwk") = 1, py::arg("fm") = false);

@@ -205,10 +205,12 @@ def tb_sweep(A, B, C, D, boxes, *, first: bool, cdom, err_i, tx, ty, tz, coefs_c
 
 
 def tbn_sweep(A, B, O0, O1, boxes, *, depth: int, first: bool, cdom, err_i, tx, ty, tz, coefs, errs,
-              rows: int = 2, waves: int = 8, chunk: int = 0, ghost: int | None = None, fma: bool = False) -> None:
+              rows: int = 2, waves: int = 8, chunk: int = 0, ghost: int | None = None, fma: bool = False,
+              delta: bool = False) -> None:
     """One deep sweep (k_tbn, ``depth`` layers u^m .. u^{m+depth-1}): the first depth-2 layers
     errors only, O0 = u^{m+depth-2}, O1 = u^{m+depth-1}. ``coefs[l]`` = (hx2, hy2, hz2, coef, ct)
-    and ``errs[l]`` the error slot of layer m+l."""
+    and ``errs[l]`` the error slot of layer m+l. ``delta``: the increment form (fp32, depth 4):
+    B = d^{m-1}, O0 = d^{m+depth-1}, O1 = u^{m+depth-1}."""
     ghost = depth if ghost is None else ghost
     gv = _check_grid_g(ghost, A, B, O0, O1)
     if ghost < depth:
@@ -216,8 +218,10 @@ def tbn_sweep(A, B, O0, O1, boxes, *, depth: int, first: bool, cdom, err_i, tx, 
     if isinstance(boxes[0], int):
         boxes = [boxes]
     bl = [_check_box_g(b, gv) for b in boxes]
-    if not _C().tbn_supported(int(depth), int(rows), int(waves), bool(fma)):
-        raise ValueError(f"unsupported depth={depth} tile rows={rows} waves={waves} fma={fma}")
+    ok = (_C().tbn_delta_supported(int(depth), int(rows), int(waves), bool(fma), A.dtype == torch.float32)
+          if delta else _C().tbn_supported(int(depth), int(rows), int(waves), bool(fma)))
+    if not ok:
+        raise ValueError(f"unsupported depth={depth} tile rows={rows} waves={waves} fma={fma} delta={delta}")
     if len(coefs) != depth or len(errs) != depth:
         raise ValueError("one coefficient set and one error slot per layer")
     for t in (tx, ty, tz):
@@ -226,7 +230,8 @@ def tbn_sweep(A, B, O0, O1, boxes, *, depth: int, first: bool, cdom, err_i, tx, 
     fn = getattr(_C(), "k_tbn_" + _sfx(A))
     fn(int(depth), int(rows), int(waves), bool(fma), bool(first), A.data_ptr(), B.data_ptr(), O0.data_ptr(),
        O1.data_ptr(), gv, bl, [int(v) for v in cdom], int(err_i[0]), int(err_i[1]), tx.data_ptr(), ty.data_ptr(),
-       tz.data_ptr(), [[float(c) for c in co] for co in coefs], [e.data_ptr() for e in errs], int(chunk), _stream())
+       tz.data_ptr(), [[float(c) for c in co] for co in coefs], [e.data_ptr() for e in errs], int(chunk), _stream(),
+       bool(delta))
 
 
 def tb3_sweep(A, B, D, E, boxes, *, first: bool, cdom, err_i, tx, ty, tz, coefs_c, coefs_d,

@@ -142,6 +142,25 @@ def chained_delta(A, Dm1, *, first: bool, mask, hx2, hy2, hz2, coefs):
     return Cf, Cf + dn, dn
 
 
+def chained_delta_layers(A, Dm1, nlayers: int, *, first: bool, mask, hx2, hy2, hz2, coefs):
+    """Increment-form deep-sweep oracle (k_tbn DELTA): d_l = d_{l-1} + c_l lap U_{l-1} (layer 0 of
+    the first sweep: c_0 lap A alone), U_l = U_{l-1} + d_l with U_{-1} = A, d_{-1} = Dm1; U and d are
+    0 where ``mask`` is False and on the outermost ring. Returns ([U_0 .. U_{n-1}], d_{n-1})."""
+    zero = torch.zeros((), dtype=A.dtype)
+    inner = (slice(1, -1),) * 3
+    m = mask.clone()
+    m[0], m[-1], m[:, 0], m[:, -1], m[:, :, 0], m[:, :, -1] = (False,) * 6
+    out, u, d = [], A, Dm1
+    for q in range(nlayers):
+        la = torch.zeros_like(u)
+        la[inner] = laplace7(u, hx2, hy2, hz2)
+        d = coefs[q] * la if (first and q == 0) else d + coefs[q] * la
+        d = torch.where(m, d, zero)
+        u = torch.where(m, u + d, zero)
+        out.append(u)
+    return out, d
+
+
 def chained_layers(A, B, nlayers: int, *, first: bool, mask, hx2, hy2, hz2, coefs):
     """Layers m, m+1, ... of a temporal-blocking sweep on full grids: C from (A, B), D from
     (C, A), E from (D, C); each layer is 0 where ``mask`` is False (Dirichlet faces) and on the

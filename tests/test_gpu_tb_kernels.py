@@ -350,6 +350,59 @@ def test_tbn_depth4_sweep_matches_reference(C, dtype, first, case):
             _check_err(errs[q], L[q][s], boxes[0], ei, tx, ty, tz, ct4[q], dtype)
 
 
+@pytest.mark.parametrize("first", [False, True])
+@pytest.mark.parametrize("case", range(len(TBN_CASES)))
+def test_tbn_depth4_delta_fp32_matches_reference(C, first, case):
+    """The fp32 increment form on four-layer sweeps (k_tbn DELTA, exact arithmetic): O0 = d of the
+    last layer, O1 = u of the last layer, and the error keys of all four layers, against the
+    chained plain-PyTorch increment-form oracle; nodes outside the boxes untouched."""
+    from wave3d.ops import kernels, reference
+
+    dtype = torch.float32
+    (X, Y, Z), boxes, cdom, chunk = TBN_CASES[case]
+    G = 4
+    shape = (X + 2 * G, Y + 2 * G, Z + 2 * G)
+    A = _rand(shape, dtype, 31)
+    Dm1 = (_rand(shape, dtype, 32) - 0.5) * 1e-3  # increments are small
+    tx, ty, tz = _tables(max(shape), dtype, 33)
+    c4 = (3.1e-4, 2.9e-4, 2.7e-4, 2.6e-4)
+    ct4 = (-0.83, 0.47, 0.21, -0.66)
+    dO0, dO1 = (torch.full(shape, v, dtype=dtype, device=DEV) for v in (-7.0, -9.0))
+    errs = [kernels.new_err(1) for _ in range(4)]
+    ei = (min(b[0] for b in boxes), max(b[1] for b in boxes))
+    co = [(*COEF.values(), c4[q], ct4[q]) for q in range(4)]
+    kernels.tbn_sweep(A.to(DEV), Dm1.to(DEV), dO0, dO1, boxes, depth=4, first=first, cdom=cdom, err_i=ei,
+                      tx=tx.to(DEV), ty=ty.to(DEV), tz=tz.to(DEV), coefs=co, errs=errs, chunk=chunk, delta=True)
+    torch.cuda.synchronize()
+    cast = lambda v: torch.tensor(v, dtype=dtype).item()  # noqa: E731
+    h = {k: cast(v) for k, v in COEF.items()}
+    L, dl = reference.chained_delta_layers(A, Dm1, 4, first=first, mask=_mask(shape, G, cdom),
+                                           coefs=[cast(c) for c in c4], **h)
+    g0, g1 = dO0.cpu(), dO1.cpu()
+    touched = torch.zeros(shape, dtype=torch.bool)
+    for b in boxes:
+        s = _sl(b, G)
+        _check(g0[s], dl[s], dtype)
+        _check(g1[s], L[3][s], dtype)
+        touched[s] = True
+    assert bool((g0[~touched] == -7.0).all()) and bool((g1[~touched] == -9.0).all())
+    if len(boxes) == 1:
+        s = _sl(boxes[0], G)
+        for q in range(4):
+            _check_err(errs[q], L[q][s], boxes[0], ei, tx, ty, tz, ct4[q], dtype)
+
+
+def test_tbn_delta_fp64_unsupported(C):
+    """No fp64 increment-form instantiation of k_tbn (register budget): refused up front."""
+    from wave3d.ops import kernels
+
+    u = torch.zeros((20, 20, 20), dtype=torch.float64, device=DEV)
+    with pytest.raises(ValueError, match="delta=True"):
+        kernels.tbn_sweep(u, u, u, u, (1, 12, 1, 12, 1, 12), depth=4, first=False, cdom=(1, 12, 1, 12), err_i=(1, 12),
+                          tx=u[0, 0], ty=u[0, 0], tz=u[0, 0], coefs=[(1, 1, 1, 0, 0)] * 4,
+                          errs=[kernels.new_err(1) for _ in range(4)], delta=True)
+
+
 @pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
 @pytest.mark.parametrize("first", [False, True])
 @pytest.mark.parametrize("case", range(len(TBN_CASES)))
