@@ -98,9 +98,11 @@ py::dict result_dict(const Config& c, const RunResult& r) {
     d["graph"] = r.graph;
     d["overlap"] = r.overlap;
     d["overlap_mode"] = r.overlap_mode;
-    d["overlap_trial_ms"] = py::make_tuple(r.overlap_trial_ms[0], r.overlap_trial_ms[1]);
-    d["overlap_trials_ms"] =
-        py::make_tuple(r.overlap_trials[0], r.overlap_trials[1], r.overlap_trials[2], r.overlap_trials[3]);
+    d["overlap_trial_ms"] = py::make_tuple(r.overlap_trial_ms[0], r.overlap_trial_ms[1], r.overlap_trial_ms[2]);
+    py::list trials;
+    for (int q = 0; q < kOverlapTrialSolves; ++q) trials.append(r.overlap_trials[q]);
+    d["overlap_trials_ms"] = py::tuple(trials);
+    d["overlap_order"] = r.overlap_order;
     d["comm_size"] = r.comm_size;
     d["rccl_max_ctas"] = r.rccl_max_ctas;
     d["halo_checked"] = r.halo_checked;

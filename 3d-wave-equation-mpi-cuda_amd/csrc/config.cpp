@@ -23,7 +23,8 @@ std::string usage() {
            "  --x-self-transport     one x rank: send the periodic wrap through the transport\n"
            "                         to this rank (exercises RCCL send/recv on a single GPU)\n"
            "  --overlap auto|on|off  interior/shell split with the halo on a second stream; auto\n"
-           "                         (default) times solves 2-5 on / off / on / off, keeps the faster\n"
+           "                         (default) times solves 2-7: on / off / on with the shells first, twice\n"
+           "                         each, and keeps the fastest\n"
            "  --no-overlap           = --overlap off\n"
            "  --kernel K             auto (leapfrog: tb4; increment form: tb3 fp32 / fma, tb2r2w4 fp64) |\n"
            "                         tb4 | tb3[r<R>w<W>] | tbn3 | tb2[r<R>][w<W>]\n"

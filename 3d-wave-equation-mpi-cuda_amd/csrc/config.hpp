@@ -36,8 +36,9 @@ struct Config {
     ICMode ic = ICMode::Ref;
     int dims[3] = {0, 0, 0};        // 0 = let dims_create choose (MPI_Dims_create semantics)
     bool overlap = true;            // interior/shell split with comm on a second stream
-    bool overlap_auto = true;       // --overlap auto (default): solves 2-5 with halos run overlap
-                                    // on / off / on / off; the arm with the faster best is kept
+    bool overlap_auto = true;       // --overlap auto (default): solves 2-7 with halos run overlap
+                                    // on / off / on with the shells first, twice each; the arm
+                                    // with the fastest best is kept
     bool json = false;              // one-line JSON summary on stdout (rank 0)
     int check_every = 0;            // >0: abort early when a layer's error is NaN/Inf/>1
     bool strict_cfl = false;        // refuse C > 1/sqrt(3)

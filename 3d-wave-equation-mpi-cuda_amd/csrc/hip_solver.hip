@@ -278,14 +278,19 @@ public:
         if (tbn_ && tbd_ == 3) res.kernel = "tbn" + res.kernel.substr(2);
         res.courant = prob_.courant;
         res.transport = ext_ ? ext_->name() : (world_ > 1 ? "loopback" : "self");
-        // --overlap auto: solves 2..5 are the trials (on, off, on, off; the first solve only warms
-        // up — first launches, RCCL connections of every message shape); the arm with the
-        // shorter best-of-two max-over-ranks solve time is kept for every later solve (one noisy
-        // sample cannot lock in the slower arm) — the same decision on every rank, since the
-        // times are reduced before the comparison
+        // --overlap auto: solves 2..7 are the trials of three arms, twice each (on with the shells
+        // beside the interior, off, on with the shells first; the first solve only warms up —
+        // first launches, RCCL connections of every message shape); the arm with the shortest
+        // best-of-two max-over-ranks solve time is kept for every later solve (one noisy sample
+        // cannot lock in a slower arm) — the same decision on every rank, since the times are
+        // reduced before the comparison. Which overlap order hides a real xGMI exchange better
+        // is the hardware's call (profiles/overlap_model_r4.txt: beside won on one GPU).
         const int trial = overlap_auto_ && solves_ >= 1 && trials_done_ < kOverlapTrials ? trials_done_ : -1;
         ++solves_;
-        if (trial >= 0) set_overlap(trial % 2 == 0);
+        if (trial >= 0) {
+            set_overlap(trial % 3 != 1);
+            shells_first_ = trial % 3 == 2;
+        }
         res.overlap = overlap_;
         res.overlap_mode = !(ext_ || world_ > 1) ? "none"
                            : overlap_auto_       ? "auto"
@@ -313,13 +318,19 @@ public:
         if (trial >= 0) {
             trial_ms_[trial] = t.total_ms;
             if (++trials_done_ == kOverlapTrials) {
-                set_overlap(best_trial(0) <= best_trial(1));
-                log_msg(LogLevel::Info, "overlap auto: on ", trial_ms_[0], "/", trial_ms_[2], " ms, off ", trial_ms_[1],
-                        "/", trial_ms_[3], " ms -> ", overlap_ ? "on" : "off");
+                int arm = 0;  // ties keep the earlier arm: on (beside), then off
+                for (int a = 1; a < 3; ++a)
+                    if (best_trial(a) < best_trial(arm)) arm = a;
+                set_overlap(arm != 1);
+                shells_first_ = arm == 2;
+                log_msg(LogLevel::Info, "overlap auto: on ", best_trial(0), " ms, off ", best_trial(1),
+                        " ms, on shells-first ", best_trial(2), " ms -> ",
+                        arm == 1 ? "off" : (arm == 2 ? "on, shells first" : "on"));
             }
         }
-        res.overlap_trial_ms[0] = best_trial(0), res.overlap_trial_ms[1] = best_trial(1);
+        for (int a = 0; a < 3; ++a) res.overlap_trial_ms[a] = best_trial(a);
         for (int q = 0; q < kOverlapTrials; ++q) res.overlap_trials[q] = trial_ms_[q];
+        res.overlap_order = shells_first_ ? "shells_first" : "beside";
         res.t = t;
         res.solve_ms.push_back(t.total_ms);
         return res;
@@ -2233,14 +2244,16 @@ private:
     bool overlap_ = false;
     bool overlap_auto_ = false;   // --overlap auto with a remote halo
     bool shells_first_ = overlap_shells_first();  // deep sweeps: shells, then exchange || interior
-    static constexpr int kOverlapTrials = 4;  // overlap auto trial solves: on, off, on, off
+    // overlap auto trial solves: on (shells beside), off, on (shells first), twice each
+    static constexpr int kOverlapTrials = kOverlapTrialSolves;
     int trials_done_ = 0;         // overlap auto trials run
     int solves_ = 0;              // solves of this session
-    double trial_ms_[kOverlapTrials] = {0, 0, 0, 0};
-    // best (smallest) trial time of an arm (0 on, 1 off) so far, 0 before its first trial
+    double trial_ms_[kOverlapTrials] = {};
+    // best (smallest) trial time of an arm (0 on beside, 1 off, 2 on shells first) so far, 0 before
+    // its first trial
     double best_trial(int arm) const {
         double b = 0;
-        for (int q = arm; q < trials_done_; q += 2) b = b > 0 ? std::min(b, trial_ms_[q]) : trial_ms_[q];
+        for (int q = arm; q < trials_done_; q += 3) b = b > 0 ? std::min(b, trial_ms_[q]) : trial_ms_[q];
         return b;
     }
     bool xself_ = false;  // --x-self-transport

@@ -98,9 +98,12 @@ std::string json_summary(const Config& c, const RunResult& r) {
       << "\", \"kernel\": \"" << r.kernel << "\", \"scheme\": \"" << r.scheme << "\", \"math\": \"" << r.math
       << "\", \"transport\": \"" << r.transport << "\""
       << ", \"overlap\": " << (r.overlap ? "true" : "false") << ", \"overlap_mode\": \"" << r.overlap_mode
-      << "\", \"overlap_trial_ms\": [" << jnum(r.overlap_trial_ms[0]) << ", " << jnum(r.overlap_trial_ms[1]) << "]"
-      << ", \"overlap_trials_ms\": [" << jnum(r.overlap_trials[0]) << ", " << jnum(r.overlap_trials[1]) << ", "
-      << jnum(r.overlap_trials[2]) << ", " << jnum(r.overlap_trials[3]) << "]"
+      << "\", \"overlap_order\": \"" << r.overlap_order << "\""
+      << ", \"overlap_trial_ms\": [" << jnum(r.overlap_trial_ms[0]) << ", " << jnum(r.overlap_trial_ms[1]) << ", "
+      << jnum(r.overlap_trial_ms[2]) << "]"
+      << ", \"overlap_trials_ms\": [";
+    for (int q = 0; q < kOverlapTrialSolves; ++q) s << (q ? ", " : "") << jnum(r.overlap_trials[q]);
+    s << "]"
       << ", \"comm_size\": " << r.comm_size << ", \"rccl_max_ctas\": " << r.rccl_max_ctas
       << ", \"halo_checked\": " << r.halo_checked
       << ", \"rccl_mirror_msgs\": " << r.rccl_mirror_msgs

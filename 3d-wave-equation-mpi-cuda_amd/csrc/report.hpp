@@ -10,6 +10,9 @@
 
 namespace wave3d {
 
+// --overlap auto: trial solves 2..7 (three arms, twice each)
+constexpr int kOverlapTrialSolves = 6;
+
 struct Timings {
     double init_ms = 0;      // allocation + table upload ("grids initialized in")
     double total_ms = 0;     // IC through last layer ("numerical solution calculated in")
@@ -40,8 +43,11 @@ struct RunResult {
     bool graph = false;  // time loop replayed as one hipGraph
     bool overlap = false;  // interior/shell split with the halo on a second stream (effective)
     std::string overlap_mode = "off";  // "on" | "off" | "auto" (requested; "none" = no halo)
-    double overlap_trial_ms[2] = {0, 0};  // --overlap auto: best trial solve time, overlap on / off
-    double overlap_trials[4] = {0, 0, 0, 0};  // every trial in order: on, off, on, off
+    // --overlap auto: best trial solve time per arm (on with the shells beside the interior, off,
+    // on with the shells first) and every trial in order (the three arms, twice)
+    double overlap_trial_ms[3] = {0, 0, 0};
+    double overlap_trials[kOverlapTrialSolves] = {};
+    std::string overlap_order = "beside";  // effective overlap order: beside | shells_first
     int comm_size = 0;     // ranks the transport's communicator reports (ncclCommCount), 0 = none
     int rccl_max_ctas = -1;  // CTA budget of the RCCL communicator (0 = RCCL's own), -1 = none
     long rccl_mirror_msgs = 0;  // --rccl-mirror: messages sent through RCCL and compared

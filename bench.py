@@ -46,7 +46,7 @@ def main() -> int:
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5, help="timed solves")
     ap.add_argument("--warmup", type=int, default=3,
-                    help="untimed solves (with halos, solves 2-5 are the --overlap auto trials)")
+                    help="untimed solves (with halos, solves 2-7 are the --overlap auto trials)")
     ap.add_argument("--N", type=int, default=0, help="override global N (default: the BASELINE config)")
     ap.add_argument("--config", default="",
                     help="run a named BASELINE config instead (models/presets.py CONFIGS, e.g. "
@@ -179,10 +179,11 @@ def main() -> int:
             dist.barrier()
 
     res = None
-    # --overlap auto with remote halos times its two arms twice each on solves 2-5 (solve 1 warms
-    # up): with fewer than 5 warm-up solves the missing trial solves run here, untimed, so the
-    # timed solves all use the chosen arm (reported as "tuning_solves")
-    tuning = (max(0, 5 - a.warmup) if a.backend == "hip" and world > 1 and not a.no_overlap
+    # --overlap auto with remote halos times its three arms (on with the shells beside the
+    # interior, off, on with the shells first) twice each on solves 2-7 (solve 1 warms up): with
+    # fewer than 7 warm-up solves the missing trial solves run here, untimed, so the timed solves
+    # all use the chosen arm (reported as "tuning_solves")
+    tuning = (max(0, 7 - a.warmup) if a.backend == "hip" and world > 1 and not a.no_overlap
               and a.overlap == "auto" else 0)
     for _ in range(tuning + a.warmup):
         res = sess.solve(args)
@@ -232,8 +233,9 @@ def main() -> int:
             "kernel": res["kernel"],
             "overlap": bool(res["overlap"]),  # effective (off when there is no remote halo)
             "overlap_mode": res.get("overlap_mode"),
-            "overlap_trial_ms": list(res.get("overlap_trial_ms", (0, 0))),  # best of two per arm
-            "overlap_trials_ms": list(res.get("overlap_trials_ms", (0, 0, 0, 0))),
+            "overlap_order": res.get("overlap_order"),  # beside | shells_first (with overlap on)
+            "overlap_trial_ms": list(res.get("overlap_trial_ms", (0, 0, 0))),  # best of two per arm
+            "overlap_trials_ms": list(res.get("overlap_trials_ms", (0,) * 6)),
             "transport": res["transport"],
             "hip_graph": bool(res.get("graph", False)),
             "fill_hbm": a.fill_hbm or None,

@@ -138,7 +138,7 @@ def test_bench_gpu_multirank_plan_staged(n, N, dims, golden):
     assert r["config"]["timesteps"] == 100 and r["linf_golden"] == golden and r["linf_ok"] is True
     assert r["halo_checked"] > 0 and r["value"] > 0
     assert r["config"]["overlap_mode"] == "auto" and min(r["config"]["overlap_trial_ms"]) > 0
-    assert r["warmup"] == 2 and r["tuning_solves"] == 3  # trial solves 3-5 ran untimed
+    assert r["warmup"] == 2 and r["tuning_solves"] == 5  # trial solves 3-7 ran untimed
     assert r["timers_ms"]["exchange_ms"] > 0 and r["timers_ms"]["comm_ms"] > 0
 
 
@@ -201,7 +201,7 @@ def test_bench_gpu_self_launch_two_ranks_staged():
     r = _bench(["--steps", "1", "--warmup", "0", "--transport", "staged", "--shared-device"], nproc=2,
                timeout=600, self_launch=True)
     _check(r, 2, 1, 0)
-    assert r["tuning_solves"] == 5  # overlap auto: warm-up + two trials per arm before the timed solve
+    assert r["tuning_solves"] == 7  # overlap auto: warm-up + two trials of each of 3 arms, then timed
     assert r["launch"] == "self" and r["config"]["N"] == 512 and r["config"]["dims"] == [2, 1, 1]
     assert r["config"]["timesteps"] == 100 and r["linf_ok"] is True
     assert r["halo_checked"] > 0

@@ -102,14 +102,21 @@ def test_rccl_mirror_every_message_shape(gpu_prog, cpu_prog, dims, kernel, dtype
 
 
 def test_overlap_auto_trials_then_keeps_the_faster(gpu_prog):
-    """--overlap auto (the default): solve 1 warms up, solves 2-5 run overlapped / not / overlapped
-    / not, later solves use the arm with the shorter best-of-two (max-over-ranks) time; the JSON
-    records every trial and the best per arm."""
-    out, _ = _run(gpu_prog, "2,2,2", "tb2", "fp64", ["--repeat", "6"])
+    """--overlap auto (the default): solve 1 warms up, solves 2-7 run the three arms twice each
+    (overlapped with the shells beside the interior / not / overlapped with the shells first),
+    later solves use the arm with the shortest best-of-two (max-over-ranks) time; the JSON records
+    every trial, the best per arm and the order kept."""
+    out, _ = _run(gpu_prog, "2,2,2", "tb4", "fp64", ["--repeat", "8"])
     assert out.returncode == 0, out.stderr[-2000:]
     r = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][0])
-    on, off = r["overlap_trial_ms"]
+    on, off, first = r["overlap_trial_ms"]
     trials = r["overlap_trials_ms"]
-    assert r["overlap_mode"] == "auto" and on > 0 and off > 0 and min(trials) > 0
-    assert on == min(trials[0], trials[2]) and off == min(trials[1], trials[3])
-    assert r["overlap"] == (on <= off)
+    assert r["overlap_mode"] == "auto" and len(trials) == 6 and min(trials) > 0
+    assert on == min(trials[0], trials[3]) and off == min(trials[1], trials[4]) and first == min(trials[2], trials[5])
+    best = min(on, off, first)  # ties keep the earlier arm
+    if on == best:
+        assert r["overlap"] and r["overlap_order"] == "beside"
+    elif off == best:
+        assert not r["overlap"]
+    else:
+        assert r["overlap"] and r["overlap_order"] == "shells_first"
