@@ -48,6 +48,11 @@
 #ifndef W3D_TB3_ONE_LDS  // A/B: 1 = the double-buffered tiles as [2] arrays (one object each)
 #define W3D_TB3_ONE_LDS 0
 #endif
+// A/B: 1 = the j neighbours of a wave's own rows that are its other own rows come from registers
+// (the centre values it already holds) instead of LDS, as k_tbn does
+#ifndef W3D_TB3_JREG
+#define W3D_TB3_JREG 1
+#endif
 #ifndef W3D_TB3_PAD
 #define W3D_TB3_PAD 0
 #endif
@@ -358,6 +363,14 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WP
     auto lapA = [&](int H, int y, int x, T ctr, T xm, T xp) {
         return lap(0, ctr, xm, xp, LA(H)[y - 1][x], LA(H)[y + 1][x], LA(H)[y][x - 1], LA(H)[y][x + 1]);
     };
+    // own row r's j neighbours: rows r-1 / r+1 of the same wave are centre values in registers
+    // (v[], as staged to LDS at (y -/+ 1, x)); the wave's edge rows read the tile
+    auto jm = [&](const T(&v)[R], int r, const auto& tile, int y, int x) {
+        return (W3D_TB3_JREG && r > 0) ? v[r > 0 ? r - 1 : 0] : tile[y - 1][x];
+    };
+    auto jp = [&](const T(&v)[R], int r, const auto& tile, int y, int x) {
+        return (W3D_TB3_JREG && r < R - 1) ? v[r < R - 1 ? r + 1 : 0] : tile[y + 1][x];
+    };
     auto cval = [&](T ctr, T bv, const auto& l) {
         if constexpr (FM) return FIRST ? ctr + lap_value(l) : l.leap(bv, kc1);
         else return FIRST ? taylor_first(ctr, l, p.coefC) : leapfrog(ctr, bv, l, p.coefC);
@@ -522,13 +535,14 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WP
 #pragma unroll
         for (int r = 0; r < R; ++r) {
             const int y = 3 + w * R + r, x = 3 + lane;
-            const auto lap = lapA(H0, y, x, a[S1][r], xpA[r], xnA[r]);
+            const auto l = lap(0, a[S1][r], xpA[r], xnA[r], jm(a[S1], r, LA(H0), y, x), jp(a[S1], r, LA(H0), y, x),
+                               LA(H0)[y][x - 1], LA(H0)[y][x + 1]);
             if constexpr (DELTA) {
-                const T dv = FIRST ? scaled(0, lap) : incr(0, bb[BC][r], lap);
+                const T dv = FIRST ? scaled(0, l) : incr(0, bb[BC][r], l);
                 dm[H0][r] = cmask(ocd[r], ocm[r], dv);
                 c[S0][r] = cmask(ocd[r], ocm[r], a[S1][r] + dv);  // FIRST: = taylor_first
             } else {
-                c[S0][r] = cmask(ocd[r], ocm[r], cval(a[S1][r], bb[BC][r], lap));
+                c[S0][r] = cmask(ocd[r], ocm[r], cval(a[S1][r], bb[BC][r], l));
             }
             LC(H0)[y - 1][x - 1] = c[S0][r];
         }
@@ -569,7 +583,7 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WP
 #pragma unroll
             for (int r = 0; r < R; ++r) {
                 const int y = 2 + w * R + r, x = 2 + lane;  // C tile coordinates
-                const auto l = lap(1, c[S3][r], cpx[r], cnx[r], LC(H1)[y - 1][x], LC(H1)[y + 1][x],
+                const auto l = lap(1, c[S3][r], cpx[r], cnx[r], jm(c[S3], r, LC(H1), y, x), jp(c[S3], r, LC(H1), y, x),
                                 LC(H1)[y][x - 1], LC(H1)[y][x + 1]);
                 if constexpr (DELTA) {
                     const T d1 = incr(1, dm[H1][r], l);  // d^{m+1}
@@ -617,8 +631,8 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WP
 #pragma unroll
             for (int r = 0; r < R; ++r) {
                 const int y = 1 + w * R + r, x = 1 + lane;  // D tile coordinates
-                const auto l = lap(2, d[S3][r], d[S2][r], d[S0][r], LD(H1)[y - 1][x], LD(H1)[y + 1][x],
-                                LD(H1)[y][x - 1], LD(H1)[y][x + 1]);
+                const auto l = lap(2, d[S3][r], d[S2][r], d[S0][r], jm(d[S3], r, LD(H1), y, x),
+                                jp(d[S3], r, LD(H1), y, x), LD(H1)[y][x - 1], LD(H1)[y][x + 1]);
                 if constexpr (DELTA) {
                     dm1[H1][r] = incr(2, dm1[H1][r], l);  // d^{m+2}
                     ev[r] = d[S3][r] + dm1[H1][r];
