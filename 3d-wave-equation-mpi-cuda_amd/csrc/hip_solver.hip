@@ -1437,8 +1437,18 @@ private:
     // same group call, bytes and stream order as a real multi-GPU rank) into a scratch buffer,
     // and a device compare against the loopback copy counts differing words per message kind:
     // every message shape of the multi-GPU plan runs through RCCL on one GPU, bit for bit.
+    // Loopback halo copies of simulated ranks: WAVE3D_LOOP_COPY=sdma issues them to the DMA
+    // engines (hipMemcpyDeviceToDeviceNoCU: no CU taken from a concurrent interior sweep, as a
+    // remote peer's xGMI traffic takes none), blit = HIP's copy kernels
+    static hipMemcpyKind loop_copy_kind() {
+        static const hipMemcpyKind k = [] {
+            const char* e = std::getenv("WAVE3D_LOOP_COPY");
+            return e && std::string(e) == "sdma" ? hipMemcpyDeviceToDeviceNoCU : hipMemcpyDeviceToDevice;
+        }();
+        return k;
+    }
     void loop_copy(void* dst, const void* src, size_t bytes, int src_rank, int dst_rank, int tag, hipStream_t s) {
-        HIP_CHECK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, s));
+        HIP_CHECK(hipMemcpyAsync(dst, src, bytes, loop_copy_kind(), s));
         if (!mirror_) return;
         W3D_REQUIRE(bytes <= mirror_bytes_, "rccl mirror scratch too small");
         mirror_->exchange({Message{0, tag, const_cast<void*>(src), bytes}}, {Message{0, tag, mirror_buf_, bytes}}, s);
