@@ -385,6 +385,29 @@ def test_tile_orders_bitwise(C, kernel):
     assert out["band"] == out["j"] == out["k"]
 
 
+def test_loop_copy_sdma_bitwise(C):
+    """Simulated ranks' loopback halo copies on the DMA engines (WAVE3D_LOOP_COPY=sdma,
+    hipMemcpyDeviceToDeviceNoCU) give the same per-layer errors as HIP's copy kernels, bit for
+    bit, on 2x1x1 and 2x2x2 with overlap off and on (read once per process: one subprocess each)."""
+    import json
+    import sys
+
+    code = ("import json, wave3d; p = wave3d.WaveProblem(48, timesteps=13, ic='shifted'); "
+            "out = [wave3d.WaveSolver(p, 'hip', ranks=P, dims=d, overlap=o).run() "
+            "for P, d in ((2, [2, 1, 1]), (8, [2, 2, 2])) for o in (False, True)]; "
+            "print(json.dumps([[r.max_abs, r.max_rel] for r in out]))")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = {}
+    for mode in ("blit", "sdma"):
+        env = dict(os.environ, WAVE3D_LOOP_COPY=mode)
+        p = subprocess.run([sys.executable, "-c", code], cwd=root, env=env, capture_output=True,
+                           text=True, timeout=120)
+        assert p.returncode == 0, p.stderr[-2000:]
+        out[mode] = json.loads(p.stdout.strip().splitlines()[-1])
+    assert out["blit"] == out["sdma"]
+    assert all(r == out["blit"][0] for r in out["blit"])
+
+
 def test_fp32_auto_is_tb4_bitwise(C):
     """fp32 leapfrog "auto" runs four-layer blocking (tb4, k_tbn r2w8): bitwise equal to the
     OpenMP fp32 oracle on one rank and on a 2x2x1 decomposition with overlap (4-deep halos)."""
