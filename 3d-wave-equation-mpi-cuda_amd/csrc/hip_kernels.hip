@@ -511,10 +511,11 @@ int march_tile_rows(const KernelVariant& v) {
 int tile_order() {
     static const int order = [] {
         const char* e = std::getenv("WAVE3D_TILE_ORDER");
-        if (!e || !*e) return 2;
-        if (e[0] == 'k') return 0;
-        if (e[0] == 'j') return 1;
-        if (e[0] == 'b') return 3;  // XCD blocks (k_tbn; the other sweeps treat it as j-fastest)
+        const std::string v = e ? e : "";
+        if (v == "k") return 0;
+        if (v == "j") return 1;
+        if (v == "blocks") return 3;  // XCD blocks (k_tbn; the other sweeps treat it as j-fastest)
+        W3D_REQUIRE(v.empty() || v == "band", "WAVE3D_TILE_ORDER must be band, blocks, j or k, not " + v);
         return 2;
     }();
     return order;
