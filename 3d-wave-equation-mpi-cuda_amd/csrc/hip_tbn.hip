@@ -48,6 +48,10 @@
 #ifndef W3D_TBN_ABL  // timing ablations (wrong results): 1 loads, 2 stores, 3 both pinned to one plane
 #define W3D_TBN_ABL 0
 #endif
+// A/B: wave priority raised (s_setprio) while a plane's prefetch loads and A staging issue
+#ifndef W3D_TBN_PRIO
+#define W3D_TBN_PRIO 0
+#endif
 #ifndef W3D_TBN_GATHER  // a layer's LDS reads ahead of its writes (1: +0.6 % fma, +1.3 % exact), and
 #define W3D_TBN_GATHER 1  // also the next layer's (2: spills at 256 VGPRs, -11 %)
 #endif
@@ -482,6 +486,7 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(1,
         constexpr int BC = P & (NB - 1), BP = (P + BDIST) & (NB - 1);  // B(i), B prefetch slots
 
         // ---- prefetch A(i+ADIST), B(i+BDIST) (own and ring; 0-record descriptors when done) --
+        if constexpr (W3D_TBN_PRIO) __builtin_amdgcn_s_setprio(W3D_TBN_PRIO);
         {
             const bool moreA = FAST || i + ADIST <= ie + D, moreB = FAST || i + BDIST <= ie + D - 1;
             // timing ablation W3D_TBN_ABL bit 0: the steady loads pinned to plane ib (wrong values)
@@ -507,6 +512,7 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(1,
         for (int s = 0; s < RP; ++s)
             if constexpr (W3D_TBN_RINGPRED) Lo(Ic<0>{}, Ic<H0>{}, sto[s]) = ra[s][S1];
             else if (rg[s]) L(Ic<0>{}, Ic<H0>{}, ry[s], rx[s]) = ra[s][S1];
+        if constexpr (W3D_TBN_PRIO) __builtin_amdgcn_s_setprio(0);
         __syncthreads();
 
         T ev[R];  // U_{D-1}(i - D + 1): stored and its errors taken below
