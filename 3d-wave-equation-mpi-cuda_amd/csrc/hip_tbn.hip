@@ -48,9 +48,10 @@
 #ifndef W3D_TBN_ABL  // timing ablations (wrong results): 1 loads, 2 stores, 3 both pinned to one plane
 #define W3D_TBN_ABL 0
 #endif
-// A/B: wave priority raised (s_setprio) while a plane's prefetch loads and A staging issue
+// A/B: wave priority raised (s_setprio) while a plane's prefetch loads and A staging issue;
+// -1 (default) = 1 for fp32 (+1-2.5 %), 0 for fp64 (+0.5 % fma, -0.6 % exact: neutral)
 #ifndef W3D_TBN_PRIO
-#define W3D_TBN_PRIO 0
+#define W3D_TBN_PRIO -1
 #endif
 #ifndef W3D_TBN_GATHER  // a layer's LDS reads ahead of its writes (1: +0.6 % fma, +1.3 % exact), and
 #define W3D_TBN_GATHER 1  // also the next layer's (2: spills at 256 VGPRs, -11 %)
@@ -58,8 +59,10 @@
 #ifndef W3D_TBN_RINGPRED  // 1: ring layers without branches (one basic block per plane), -1.6 %
 #define W3D_TBN_RINGPRED 0
 #endif
-#ifndef W3D_TBN_ONE_LDS  // 1: all staged tiles in one __shared__ array (-1 %)
-#define W3D_TBN_ONE_LDS 0
+// 1: all staged tiles in one __shared__ array (fp64 -1 %, fp32 +1-5 %), 0: one object per tile,
+// 2 (default): one array for fp32, objects for fp64 (profiles/deep_sweeps_r4.txt batches 21/30)
+#ifndef W3D_TBN_ONE_LDS
+#define W3D_TBN_ONE_LDS 2
 #endif
 #ifndef W3D_TBN_MASKMUL  // face masks and the fma checksum as products (see cmask; 0: selects, -3 %)
 #define W3D_TBN_MASKMUL 1
@@ -161,26 +164,22 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(1,
     // Every staged (layer, buffer) tile is its own __shared__ object: distinct objects cannot
     // alias, so the compiler may hoist a layer's LDS reads above the previous layer's LDS
     // writes (other tiles) instead of issuing read -> wait -> compute -> write one layer at a
-    // time (one array with computed offsets serialised them, W3D_TBN_ONE_LDS)
-#if W3D_TBN_ONE_LDS
-    __shared__ T lds[Gm::total];
-    auto Lo = [&](auto sc, auto hc, int o) -> T& {
-        constexpr int s = decltype(sc)::value, h = decltype(hc)::value;
-        return lds[Gm::off(s) + h * Gm::size(s) + o];
-    };
-#else
+    // time (one array with computed offsets serialised them, W3D_TBN_ONE_LDS). fp32 runs faster
+    // with the one array (W3D_TBN_ONE_LDS = 2, the default: fp64 objects, fp32 one array)
+    constexpr bool ONE = W3D_TBN_ONE_LDS == 1 || (W3D_TBN_ONE_LDS == 2 && sizeof(T) == 4);
+    __shared__ T lds[ONE ? Gm::total : 1];
     constexpr int Z0 = Gm::size(0), Z1 = Gm::size(1), Z2 = Gm::size(D > 2 ? 2 : 1), Z3 = Gm::size(D > 3 ? 3 : 1);
-    __shared__ T t00[Z0], t01[Z0], t10[Z1], t11[Z1], t20[D > 2 ? Z2 : 1], t21[D > 2 ? Z2 : 1],
-        t30[D > 3 ? Z3 : 1], t31[D > 3 ? Z3 : 1];
+    constexpr int Y0 = ONE ? 1 : Z0, Y1 = ONE ? 1 : Z1, Y2 = ONE || D <= 2 ? 1 : Z2, Y3 = ONE || D <= 3 ? 1 : Z3;
+    __shared__ T t00[Y0], t01[Y0], t10[Y1], t11[Y1], t20[Y2], t21[Y2], t30[Y3], t31[Y3];
     // staged layer s, buffer h, offset o in its frame
     auto Lo = [&](auto sc, auto hc, int o) -> T& {
         constexpr int s = decltype(sc)::value, h = decltype(hc)::value;
-        if constexpr (s == 0) return h ? t01[o] : t00[o];
+        if constexpr (ONE) return lds[Gm::off(s) + h * Gm::size(s) + o];
+        else if constexpr (s == 0) return h ? t01[o] : t00[o];
         else if constexpr (s == 1) return h ? t11[o] : t10[o];
         else if constexpr (s == 2) return h ? t21[o] : t20[o];
         else return h ? t31[o] : t30[o];
     };
-#endif
     // ... at A-frame coordinates (y, x)
     auto L = [&](auto sc, auto hc, int y, int x) -> T& { return Lo(sc, hc, Gm::at(decltype(sc)::value, y, x)); };
 
@@ -486,7 +485,8 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(1,
         constexpr int BC = P & (NB - 1), BP = (P + BDIST) & (NB - 1);  // B(i), B prefetch slots
 
         // ---- prefetch A(i+ADIST), B(i+BDIST) (own and ring; 0-record descriptors when done) --
-        if constexpr (W3D_TBN_PRIO) __builtin_amdgcn_s_setprio(W3D_TBN_PRIO);
+        constexpr int PRIO = W3D_TBN_PRIO >= 0 ? W3D_TBN_PRIO : (sizeof(T) == 4 ? 1 : 0);
+        if constexpr (PRIO) __builtin_amdgcn_s_setprio(PRIO);
         {
             const bool moreA = FAST || i + ADIST <= ie + D, moreB = FAST || i + BDIST <= ie + D - 1;
             // timing ablation W3D_TBN_ABL bit 0: the steady loads pinned to plane ib (wrong values)
@@ -512,7 +512,7 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(1,
         for (int s = 0; s < RP; ++s)
             if constexpr (W3D_TBN_RINGPRED) Lo(Ic<0>{}, Ic<H0>{}, sto[s]) = ra[s][S1];
             else if (rg[s]) L(Ic<0>{}, Ic<H0>{}, ry[s], rx[s]) = ra[s][S1];
-        if constexpr (W3D_TBN_PRIO) __builtin_amdgcn_s_setprio(0);
+        if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
         __syncthreads();
 
         T ev[R];  // U_{D-1}(i - D + 1): stored and its errors taken below
