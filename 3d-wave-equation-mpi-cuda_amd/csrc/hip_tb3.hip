@@ -48,6 +48,10 @@
 #ifndef W3D_TB3_ONE_LDS  // A/B: 1 = the double-buffered tiles as [2] arrays (one object each)
 #define W3D_TB3_ONE_LDS 0
 #endif
+// A/B: wave priority raised (s_setprio) while a plane's prefetch loads and A staging issue
+#ifndef W3D_TB3_PRIO
+#define W3D_TB3_PRIO 0
+#endif
 // A/B: 1 = the j neighbours of a wave's own rows that are its other own rows come from registers
 // (the centre values it already holds) instead of LDS, as k_tbn does
 #ifndef W3D_TB3_JREG
@@ -466,6 +470,7 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WP
         constexpr int BC = P & (NB - 1), BP = (P + BD) & (NB - 1);  // B(i), B(i+BD) slots
 
         // ---- prefetch A(i+2), B(i+BD) (own and ring; 0-record descriptors when done) -------
+        if constexpr (W3D_TB3_PRIO > 0) __builtin_amdgcn_s_setprio(W3D_TB3_PRIO);
         {
             const bool more = FAST || i <= ie + 1, moreB = FAST || i + BD <= ie + 2;
             const unsigned nb = more ? pbytes : 0u;
@@ -489,6 +494,7 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WP
 #pragma unroll
         for (int s = 0; s < RP; ++s)
             if (rg[s]) LA(H0)[ry[s]][rx[s]] = ra[s][S1];
+        if constexpr (W3D_TB3_PRIO > 0) __builtin_amdgcn_s_setprio(0);
         __syncthreads();
 
         // ---- seam partners (uniform branch, rare) -------------------------------------------
