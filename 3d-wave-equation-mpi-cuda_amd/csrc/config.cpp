@@ -26,7 +26,7 @@ std::string usage() {
            "                         (default) times solves 2-7: on / off / on with the shells first, twice\n"
            "                         each, and keeps the fastest\n"
            "  --no-overlap           = --overlap off\n"
-           "  --kernel K             auto (leapfrog: tb4; increment form: tb3 fp32 / fma, tb2r2w4 fp64) |\n"
+           "  --kernel K             auto (leapfrog: tb4; increment form: tb3) |\n"
            "                         tb4 | tb3[r<R>w<W>] | tbn3 | tb2[r<R>][w<W>]\n"
            "                         | march[2|4|8][nt|p|f]\n"
            "                         | naive | flat   (temporal blocking / single-step variants)\n"

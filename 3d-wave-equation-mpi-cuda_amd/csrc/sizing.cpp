@@ -41,13 +41,15 @@ Layout plan_layout(const Config& c, int world) {
     // errors of three layers per table row) the 16-row r2w8 tile (2 waves/SIMD) beats the
     // 1-row r1w8 (4 waves/SIMD): 425-431k vs 402k Mpts/s at N=512 (profiles/tb3_salu_r3.txt)
     // fp64 exact leapfrog: tb3 too since the scalar diet — 373-374k vs tb2r2w8 317k Mpts/s at
-    // N=512, bitwise equal (profiles/tb3_salu_r3.txt); the fp64 increment form stays on tb2r2w4
+    // N=512, bitwise equal (profiles/tb3_salu_r3.txt)
     // Since round 4 the leapfrog (fp64 and fp32, exact and FMA) runs four layers per sweep (tb4,
     // k_tbn r2w8: 8 B per node-layer instead of 10.7): fp64 fma 521-528k vs tb3 428-435k, exact
     // 433k vs 374k, fp32 fma 794k vs 791k, fp32 exact 825k vs 717k Mpts/s at N=512 K=100
-    // (profiles/deep_sweeps_r4.txt). k_tbn has no increment form: fp32 / fp64-fma delta stay on tb3.
+    // (profiles/deep_sweeps_r4.txt). The increment form runs on tb3 (k_tbn's fp32 one is slower),
+    // since round 4 the fp64 exact one too: 378-379k vs tb2r2w4 298k Mpts/s at N=512 after tb3's
+    // register j-neighbours and the max-ilp build (deep_sweeps_r4.txt batch 33).
     const bool auto_tb4 = auto_tb && !c.delta;
-    const bool auto_tb3 = auto_tb && !auto_tb4 && (c.dtype == DType::F32 || c.fma);
+    const bool auto_tb3 = auto_tb && !auto_tb4;
     const bool tbn3 = c.kernel.rfind("tbn3", 0) == 0;  // k_tbn at depth 3 (A/B of k_tb3)
     const bool tb4 = auto_tb4 || c.kernel.rfind("tb4", 0) == 0;
     const bool tb3 = !tb4 && (auto_tb3 || tbn3 || c.kernel.rfind("tb3", 0) == 0);

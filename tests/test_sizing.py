@@ -33,9 +33,9 @@ def test_bytes_per_rank_matches_level_formula(C):
     assert p32["tb"] and p32["ghost"] == 4 and p32["levels"] == 4
     b32 = p32["bytes_per_rank"]
     assert 0.50 * b < b32 < 0.56 * b
-    # the fp64 increment form keeps two-layer blocking (4 levels, 2-deep ghosts)
+    # the fp64 increment form: three-layer blocking (tb3, 4 levels, 3-deep ghosts)
     pd = C.memory_plan(ARGS + ["--scheme", "delta"], 1)
-    assert pd["ghost"] == 2 and pd["levels"] == 4
+    assert pd["ghost"] == 3 and pd["levels"] == 4
     # the fp32 increment form: three-layer blocking (tb3, no tb4 increment form), 3-deep ghosts
     p32d = C.memory_plan(ARGS + ["--dtype", "fp32", "--scheme", "delta"], 1)
     assert p32d["ghost"] == 3 and p32d["levels"] == 4 and p32d["bytes_per_rank"] < b32
