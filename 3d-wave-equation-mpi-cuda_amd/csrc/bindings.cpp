@@ -103,6 +103,7 @@ py::dict result_dict(const Config& c, const RunResult& r) {
     for (int q = 0; q < kOverlapTrialSolves; ++q) trials.append(r.overlap_trials[q]);
     d["overlap_trials_ms"] = py::tuple(trials);
     d["overlap_order"] = r.overlap_order;
+    d["overlap_order_run"] = r.overlap_order_run;
     d["comm_size"] = r.comm_size;
     d["rccl_max_ctas"] = r.rccl_max_ctas;
     d["halo_checked"] = r.halo_checked;

@@ -180,7 +180,7 @@ __device__ __forceinline__ void commit_errors(T ma, T mr, T chk, u64* err) {
 // (blockIdx % 8), each with its own L2. Renumbering so that XCD x runs one contiguous range
 // of logical tiles keeps k- and j-neighbour tiles — which read each other's edge rows and
 // columns as halo — on the same L2 instead of always on different ones. Measured on
-// MI355X (profiles/sweep_n512_xcd_swizzle_r1.txt) it does not pay here (halo lines come
+// MI355X (profiles/sweep_n512_tb_variants_r1.txt) it does not pay here (halo lines come
 // from the memory-side Infinity Cache either way), so it is opt-in: WAVE3D_XCD_SWIZZLE=1.
 constexpr int kXcds = 8;
 __device__ __forceinline__ int xcd_swizzle(int bid, int total, bool on) {

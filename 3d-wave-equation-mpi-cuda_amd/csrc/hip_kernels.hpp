@@ -147,7 +147,7 @@ struct TbnSeam {
     const T* nP[kTbnMaxDepth - 1] = {};
     const T* pP[kTbnMaxDepth - 1] = {};
 };
-bool tbn_supported(int depth, int rows, int waves, bool fm);
+bool tbn_supported(int depth, int rows, int waves, bool fm, bool fp32);
 // the increment form (DELTA): fp32 at depth 4 only
 bool tbn_delta_supported(int depth, int rows, int waves, bool fm, bool fp32);
 template <class T>

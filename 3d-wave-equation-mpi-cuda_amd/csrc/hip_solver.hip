@@ -171,7 +171,7 @@ public:
         L_ = lay.L;
         for (int a = 0; a < 3; ++a) cfg_.dims[a] = lay.dims[a];
         W3D_REQUIRE(tbd_ < 4 || (c.delta ? tbn_delta_supported(4, tb_rows_, tb_waves_, c.fma, c.dtype == DType::F32)
-                                         : tbn_supported(4, tb_rows_, tb_waves_, c.fma)),
+                                         : tbn_supported(4, tb_rows_, tb_waves_, c.fma, c.dtype == DType::F32)),
                     "four-layer blocking: tile r2w8; the increment form in fp32 only");
         W3D_REQUIRE(!c.fma || !tb_ || tbd_ == 4 ||
                         (tbd_ == 3 ? (c.delta ? tb3_delta_supported(tb_rows_, tb_waves_, true)
@@ -179,7 +179,7 @@ public:
                                    : tb_occ_ == 0 && tb2_fma_supported(tb_rows_, tb_waves_, tb_nwk_, c.delta)),
                     "--math fma: no fma instantiation of this temporal-blocking tile (tb3, tb3r1w8, tb3r1w16, "
                     "tb2r2w8, tb2)");
-        W3D_REQUIRE(!tbn_ || tbd_ == 4 || (!c.delta && tbn_supported(3, tb_rows_, tb_waves_, c.fma)),
+        W3D_REQUIRE(!tbn_ || tbd_ == 4 || (!c.delta && tbn_supported(3, tb_rows_, tb_waves_, c.fma, c.dtype == DType::F32)),
                     "tbn3: leapfrog, tile r2w8");
         W3D_REQUIRE(!tb_ || tbd_ == 4 || (tbd_ == 3 ? tb3_supported(tb_rows_, tb_waves_)
                                         : tb2_supported(tb_rows_, tb_waves_, tb_occ_, tb_nwk_)),
@@ -287,10 +287,7 @@ public:
         // is the hardware's call (profiles/overlap_model_r4.txt: beside won on one GPU).
         const int trial = overlap_auto_ && solves_ >= 1 && trials_done_ < kOverlapTrials ? trials_done_ : -1;
         ++solves_;
-        if (trial >= 0) {
-            set_overlap(trial % 3 != 1);
-            shells_first_ = trial % 3 == 2;
-        }
+        if (trial >= 0) set_overlap(trial % 3 != 1, trial % 3 == 2);
         res.overlap = overlap_;
         res.overlap_mode = !(ext_ || world_ > 1) ? "none"
                            : overlap_auto_       ? "auto"
@@ -321,8 +318,7 @@ public:
                 int arm = 0;  // ties keep the earlier arm: on (beside), then off
                 for (int a = 1; a < 3; ++a)
                     if (best_trial(a) < best_trial(arm)) arm = a;
-                set_overlap(arm != 1);
-                shells_first_ = arm == 2;
+                set_overlap(arm != 1, arm == 2);
                 log_msg(LogLevel::Info, "overlap auto: on ", best_trial(0), " ms, off ", best_trial(1),
                         " ms, on shells-first ", best_trial(2), " ms -> ",
                         arm == 1 ? "off" : (arm == 2 ? "on, shells first" : "on"));
@@ -330,7 +326,8 @@ public:
         }
         for (int a = 0; a < 3; ++a) res.overlap_trial_ms[a] = best_trial(a);
         for (int q = 0; q < kOverlapTrials; ++q) res.overlap_trials[q] = trial_ms_[q];
-        res.overlap_order = shells_first_ ? "shells_first" : "beside";
+        res.overlap_order = !overlap_ ? "none" : shells_first_ ? "shells_first" : "beside";
+        res.overlap_order_run = order_enqueued_;
         res.t = t;
         res.solve_ms.push_back(t.total_ms);
         return res;
@@ -603,9 +600,16 @@ private:
     }
 
     // ---- helpers ----------------------------------------------------------------------
-    // the enqueue order depends on overlap_: a captured graph of the other arm is dropped
-    void set_overlap(bool on) {
-        if (on == overlap_) return;
+    // the enqueue order depends on overlap_ and shells_first_: a captured graph of another arm
+    // (either field) is dropped
+    void set_overlap(bool on, bool shells_first) {
+        if (on == overlap_ && shells_first == shells_first_) return;
+        shells_first_ = shells_first;
+        if (on == overlap_) {
+            if (gexec_) (void)hipGraphExecDestroy(gexec_);
+            gexec_ = nullptr;
+            return;
+        }
         overlap_ = on;
         // between solves (both streams idle): the sweeps move to the CU-masked stream and back
         if (s_comp_cu_) s_comp_ = on ? s_comp_cu_ : s_comp_full_;
@@ -1822,6 +1826,9 @@ private:
     // Returns the last layer computed.
     int enqueue_layers(RunResult& res, int start) {
         TraceRange tr("wave3d.layers");
+        // the order this enqueue (or the graph captured from it) runs: checked against the
+        // reported order by tests (a replayed graph of another arm would show here)
+        order_enqueued_ = !overlap_ ? "none" : shells_first_ ? "shells_first" : "beside";
         CuReserveScope cu_scope(s_comp_ == s_comp_cu_ ? comm_cus_ : 0);  // work items for the CUs kept
         const int K = prob_.K;
         int done = start - 1;
@@ -2246,6 +2253,7 @@ private:
     int tbd_ = 1;       // layers per sweep (1, 2, 3 or 4)
     bool tbn_ = false;  // deep sweeps through k_tbn (tb4; "tbn3": the depth-generic kernel at 3)
     hipGraphExec_t gexec_ = nullptr;  // captured IC + time loop (graph_eligible())
+    const char* order_enqueued_ = "none";  // overlap order of the last enqueue / captured graph
     bool graph_failed_ = false;
     int G_ = 1;         // ghost depth
     int L_ = 3;         // time levels kept

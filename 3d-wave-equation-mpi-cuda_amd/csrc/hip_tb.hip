@@ -82,7 +82,7 @@ struct TbParams {
 // ABL (measurement ablation, env WAVE3D_TB_ABLATION, not a solver mode): 1 = no error
 // reduction at all, 2 = absolute error only (no relative-error division).
 // C and D are written with the non-temporal policy (+3-5 % at N=512,
-// profiles/sweep_tb2_cache_policy_r1.txt). OPT (env WAVE3D_TB_OPT, A/B ablation, bitwise-
+// profiles/sweep_store_policy_r1.txt). OPT (env WAVE3D_TB_OPT, A/B ablation, bitwise-
 // neutral): 1 = default-policy stores instead. (Prefetch distances: own A and both A rings 2
 // planes, B 1 plane; B at distance 2 measured no faster, the outer ring at distance 2 +2.6 %.)
 // DELTA: increment form (csrc/hip_kernels.hpp launch_tb2): B = d^{m-1}; d^m = B + coefC*lap A,

@@ -9,25 +9,31 @@
 // Workgroup = NW wave64s owning a (NW*R rows) x 64 tile of U_{D-1} that marches along i. Layer
 // l is evaluated l planes behind layer 0, on a (D-1-l)-node ring around the tile (redundantly
 // with the neighbour tiles; identical operations, so bitwise equal):
-//   iteration i:  stage A(i) (tile + D-ring) -> barrier
+//   iteration i:  wait for A(i+1), B(i) -> barrier -> LDS-DMA of B(i+1), A(i+2)
 //                 U_0(i)       on tile + (D-1)-ring  from A(i-1..i+1), B(i)
 //                 U_l(i - l)   on tile + (D-1-l)-ring from U_{l-1} (staged last iteration) and
 //                              U_{l-2} (A for l = 1) of the same plane
-// Every staged tile is double-buffered, so one barrier per plane. Register state sits in slots
-// indexed by plane number mod 4 / mod 2 with the i loop unrolled by 4 (no copies of in-flight
-// loads): U_l(x) lives in slot (x + l - i0) & 3, i.e. the phase of the iteration that made it.
 //
-// Ring ownership (as k_tb3): every ring node belongs to ONE thread, RP positions per thread, in
-// the order rings 1..D-2 whole, ring D-1 without its corners (no later layer reads layer 0
-// there), then the staging-only positions: the four ring-(D-1) corners (A there is read by layer
-// 0 on the adjacent ring-(D-1) nodes) and ring D without corners. With 16-row tiles the compute
-// positions of D = 4 are exactly 512 (one per thread of 8 waves), so the second slot only
-// stages A. A slot whose first possible ring is r only carries the history of the layers
-// evaluated on ring r (compile-time), so the far rings cost registers for A and B only.
+// Staging (gfx950 LDS-DMA, buffer_load_dword ... lds): A and B never pass through VGPRs. Every
+// A plane (tile + D-ring: (TJ+2D) x (64+2D) values) lands in a 4-slot LDS ring, every B plane
+// (tile + (D-1)-ring) in a 2-slot ring, each row as 256-B pieces (64 lanes x 4 B, lane-linear
+// into the odd-pitch frame row); all of a plane's A/B reads — centre, x+-1 planes, y/z
+// neighbours — are LDS reads. The loads are invisible to the compiler (inline asm), so its own
+// s_waitcnt never drains them; each iteration waits with a counted vmcnt for the pieces issued
+// one iteration earlier (the stores issued after them stay in flight) and crosses one barrier.
+// Compared with register staging (round 4: 248 VGPRs, A/B prefetch slots + ds_write of A) this
+// frees the prefetch registers and the staging writes, and the ring's column halos are read as
+// rows (256-B pieces) instead of one 8-B lane per row.
 //
-// Load pipeline depth (DEEP bits): bit 0 — A is prefetched three planes ahead instead of two: A(i-1)
-// is read from the LDS tile staged last iteration (still intact until the next barrier), so its
-// register slot takes A(i+3) at the top of the iteration; bit 1 — B two planes ahead (4 slots).
+// The U frames are double-buffered (layer l reads U_{l-1} of the last iteration while writing
+// its own), so one barrier per plane. Register state sits in slots indexed by plane number mod
+// 4 with the i loop unrolled by 4 (no copies): U_l(x) lives in slot (x + l - i0) & 3.
+//
+// Ring ownership (as k_tb3): every computed ring node belongs to ONE thread, RP positions per
+// thread, in the order rings 1..D-2 whole, ring D-1 without its corners (no later layer reads
+// layer 0 there). With 16-row tiles the positions of D = 4 are exactly 512 (one per thread of
+// 8 waves). A slot whose first possible ring is r only carries the history of the layers
+// evaluated on ring r (compile-time).
 //
 // Periodic seam (the reference keeps both x = 0 and x = N, mpi_new.cpp:170-176): at plane an_i
 // (the ghost copy of global N-1) the x+ neighbour of layer l is the partner plane nP[l] — A at
@@ -43,30 +49,6 @@
 #include <utility>
 
 #include "device_common.hpp"
-
-// Build-time A/B switches, measured in profiles/deep_sweeps_r4.txt (the defaults are the winners):
-#ifndef W3D_TBN_ABL  // timing ablations (wrong results): 1 loads, 2 stores, 3 both pinned to one plane
-#define W3D_TBN_ABL 0
-#endif
-// A/B: wave priority raised (s_setprio) while a plane's prefetch loads and A staging issue;
-// -1 (default) = 1 for fp32 (+1-2.5 %), 0 for fp64 (+0.5 % fma, -0.6 % exact: neutral)
-#ifndef W3D_TBN_PRIO
-#define W3D_TBN_PRIO -1
-#endif
-#ifndef W3D_TBN_GATHER  // a layer's LDS reads ahead of its writes (1: +0.6 % fma, +1.3 % exact), and
-#define W3D_TBN_GATHER 1  // also the next layer's (2: spills at 256 VGPRs, -11 %)
-#endif
-#ifndef W3D_TBN_RINGPRED  // 1: ring layers without branches (one basic block per plane), -1.6 %
-#define W3D_TBN_RINGPRED 0
-#endif
-// 1: all staged tiles in one __shared__ array (fp64 -1 %, fp32 +1-5 %), 0: one object per tile,
-// 2 (default): one array for fp32, objects for fp64 (profiles/deep_sweeps_r4.txt batches 21/30)
-#ifndef W3D_TBN_ONE_LDS
-#define W3D_TBN_ONE_LDS 2
-#endif
-#ifndef W3D_TBN_MASKMUL  // face masks and the fma checksum as products (see cmask; 0: selects, -3 %)
-#define W3D_TBN_MASKMUL 1
-#endif
 
 namespace wave3d {
 namespace {
@@ -115,73 +97,172 @@ struct TbnParams {
     u64* err[kTbnMaxDepth];
 };
 
-// Tile geometry of a D-layer sweep over TJ x 64 tiles (coordinates in the "A frame": row y =
-// j - jt + D, column x = k - kb + D).
-template <int D, int TJ>
+// Tile geometry of a D-layer sweep over TJ x 64 tiles of ES-byte values on NW waves
+// (coordinates in the "A frame": row y = j - jt + D, column x = k - kb + D).
+template <int D, int TJ, int ES, int NW>
 struct TbnGeom {
     // staged layer s: 0 = A (ring D), s >= 1 = U_{s-1} (ring D - s); frame origin (s, s)
     static constexpr int H(int s) { return TJ + 2 * (D - s); }
-    // row pitch: the staged width rounded up to odd, so the lanes of a ring column (one k,
-    // consecutive rows) hit 32 distinct ds_read_b64 bank pairs (an even pitch of 72 doubles put
-    // 8 rows on one pair: 4.6x the bank-conflict cycles of k_tb3 in the first tb4 PMC)
-    static constexpr int W(int s) { return (kTK + 2 * (D - s)) | 1; }
+    // row pitch of the U frames (ds_write): the staged width rounded up to odd, so the lanes of
+    // a ring column (one k, consecutive rows) hit 32 distinct ds_read_b64 bank pairs (an even
+    // pitch of 72 doubles put 8 rows on one pair: 4.6x the bank-conflict cycles of k_tb3 in the
+    // first tb4 PMC). The A / B slots (LDS-DMA) of fp64 take whole 16-B pieces per lane, so
+    // their pitch is even: 2 mod 4 doubles (20 r mod 64 banks: 16 distinct pairs, a 2-way
+    // conflict on 32-row column reads at most); fp32 slots keep the odd pitch (dword pieces).
+    static constexpr int W(int s) {
+        return s > 0 || ES != 8 ? (kTK + 2 * (D - s)) | 1 : (kTK + 2 * D) % 4 == 2 ? kTK + 2 * D : kTK + 2 * D + 2;
+    }
     static constexpr int cells(int s) { return H(s) * W(s); }
-    static constexpr int size(int s) { return cells(s) + 1; }  // + a trash cell (predicated ring writes)
     static constexpr int at(int s, int y, int x) { return (y - s) * W(s) + (x - s); }
-    static constexpr int off(int s) { return s == 0 ? 0 : off(s - 1) + 2 * size(s - 1); }
-    static constexpr int total = off(D);
-    // positions of "ring" r: rings 1..D-2 whole, D-1 without corners, D = the 4 corners of ring
-    // D-1 plus ring D without corners (staging only)
+    // A and B (= u^{m-2}, read by layer 0 on the tile + (D-1)-ring only) slots: the A frame
+    // rounded up to RPW rows per wave (the rows past the frame are loaded and never read)
+    static constexpr int RPW = (H(0) + NW - 1) / NW;
+    static constexpr int scells = RPW * NW * W(0);
+    static constexpr int rowb = (kTK + 2 * D) * ES;  // bytes a row's DMA moves
+    // one-array layout (fp32): A slots 0..3, B slots 0..1, then U_{s-1} frames x 2 buffers
+    static constexpr int a_off(int q) { return q * scells; }
+    static constexpr int b_off(int q) { return (4 + q) * scells; }
+    static constexpr int u_off(int s, int h) {
+        return s == 1 ? b_off(2) + h * cells(1) : u_off(s - 1, 1) + cells(s - 1) + h * cells(s);
+    }
+    static constexpr int total = u_off(D - 1, 1) + cells(D - 1);
+    // computed positions of ring r: rings 1..D-2 whole, D-1 without corners
     static constexpr int npos(int r) {
-        return 2 * (kTK + 2 * (r - 1)) + 2 * (TJ + 2 * (r - (r >= D - 1 ? 1 : 0))) + (r == D ? 4 : 0);
+        return 2 * (kTK + 2 * (r - 1)) + 2 * (TJ + 2 * (r - (r == D - 1 ? 1 : 0)));
     }
     static constexpr int first(int r) { return r <= 1 ? 0 : first(r - 1) + npos(r - 1); }
-    static constexpr int nall = first(D + 1);
-    // ring of ring position q (D + 1: none)
+    static constexpr int ncomp = first(D);
+    // ring of position q (D: none)
     static constexpr int ring_of(int q) {
         int r = 1;
-        while (r <= D && q >= first(r + 1)) ++r;
+        while (r < D && q >= first(r + 1)) ++r;
         return r;
     }
 };
+
+// LDS byte address of a __shared__ object (the DMA destination base in M0)
+template <class T>
+__device__ __forceinline__ unsigned lds_addr(T* ptr) {
+    return static_cast<unsigned>(reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) T*)ptr));
+}
+// LDS-DMA fill of a wave's three consecutive slot rows (probed on gfx950, tools/microbench/
+// lds_dma_probe.hip: the destination is M0 + instruction offset + size * lane, the source moves
+// by the instruction offset too, out-of-range lanes write 0, masked lanes nothing). Row q: source
+// src0 + q sjb (+ lane piece), LDS slot + lds0 + q ROWB.
+//   fp64: one buffer_load_dwordx4 per row (rowb / 16 lanes, 16 B each: the even slot pitch);
+//   fp32: two buffer_load_dword per row (256 B, then the rowb - 256 B tail; odd pitch).
+// One asm statement per fill, so hipcc neither counts nor drains the pieces (vmcnt is ours:
+// vm_wait) and nothing per row is hoisted into SGPRs. M0 is written in the statement that reads
+// it (hipcc keeps nothing in M0 in these kernels: no M0 use outside these statements); the
+// s_add's write SCC, declared clobbered (or hipcc may split a 64-bit s_add_u32 / s_addc_u32 pair,
+// a plane descriptor's base, around the statement).
+template <int ES, int ROWB, int RB>
+__device__ __forceinline__ void dma_fill3(__amdgpu_buffer_rsrc_t r, unsigned src0, unsigned sjb, unsigned slot,
+                                          unsigned lds0) {
+    unsigned v0, v1, v2;
+    u64 keep;
+    const unsigned lane = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+    if constexpr (ES == 8) {
+        static_assert(RB % 16 == 0 && RB <= 1024, "fp64 rows: one dwordx4 piece per lane");
+        asm volatile(
+            "s_add_u32 m0, %[slot], %[lds0]\n\t"
+            "v_add_u32 %[v0], %[src0], %[l16]\n\t"
+            "v_add_u32 %[v1], %[sjb], %[v0]\n\t"
+            "v_add_u32 %[v2], %[sjb], %[v1]\n\t"
+            "s_mov_b64 %[keep], exec\n\t"
+            "s_mov_b64 exec, %[mask]\n\t"
+            "buffer_load_dwordx4 %[v0], %[rs], 0 offen lds\n\t"
+            "s_add_u32 m0, m0, %[rowb]\n\t"
+            "s_nop 0\n\t"
+            "buffer_load_dwordx4 %[v1], %[rs], 0 offen lds\n\t"
+            "s_add_u32 m0, m0, %[rowb]\n\t"
+            "s_nop 0\n\t"
+            "buffer_load_dwordx4 %[v2], %[rs], 0 offen lds\n\t"
+            "s_mov_b64 exec, %[keep]"
+            : [v0] "=&v"(v0), [v1] "=&v"(v1), [v2] "=&v"(v2), [keep] "=&s"(keep)
+            : [slot] "s"(slot), [lds0] "s"(lds0), [src0] "s"(src0), [sjb] "s"(sjb), [l16] "v"(16u * lane),
+              [rs] "s"(r), [rowb] "i"(ROWB), [mask] "s"(u64(RB / 16 >= 64 ? ~0ull : (1ull << (RB / 16)) - 1))
+            : "memory", "scc");
+    } else {
+        static_assert(RB > 256 && RB <= 512 && RB % 4 == 0, "fp32 rows: 256 B + a tail");
+        asm volatile(
+            "s_add_u32 m0, %[slot], %[lds0]\n\t"
+            "v_add_u32 %[v0], %[src0], %[l4]\n\t"
+            "v_add_u32 %[v1], %[sjb], %[v0]\n\t"
+            "v_add_u32 %[v2], %[sjb], %[v1]\n\t"
+            "buffer_load_dword %[v0], %[rs], 0 offen lds\n\t"
+            "s_add_u32 m0, m0, %[rowb]\n\t"
+            "s_nop 0\n\t"
+            "buffer_load_dword %[v1], %[rs], 0 offen lds\n\t"
+            "s_add_u32 m0, m0, %[rowb]\n\t"
+            "s_nop 0\n\t"
+            "buffer_load_dword %[v2], %[rs], 0 offen lds\n\t"
+            "s_mov_b64 %[keep], exec\n\t"
+            "s_mov_b64 exec, %[mask]\n\t"
+            "buffer_load_dword %[v2], %[rs], 0 offen offset:256 lds\n\t"
+            "s_sub_u32 m0, m0, %[rowb]\n\t"
+            "s_nop 0\n\t"
+            "buffer_load_dword %[v1], %[rs], 0 offen offset:256 lds\n\t"
+            "s_sub_u32 m0, m0, %[rowb]\n\t"
+            "s_nop 0\n\t"
+            "buffer_load_dword %[v0], %[rs], 0 offen offset:256 lds\n\t"
+            "s_mov_b64 exec, %[keep]"
+            : [v0] "=&v"(v0), [v1] "=&v"(v1), [v2] "=&v"(v2), [keep] "=&s"(keep)
+            : [slot] "s"(slot), [lds0] "s"(lds0), [src0] "s"(src0), [sjb] "s"(sjb), [l4] "v"(4u * lane),
+              [rs] "s"(r), [rowb] "i"(ROWB), [mask] "s"(u64((1ull << ((RB - 256) / 4)) - 1))
+            : "memory", "scc");
+    }
+}
+template <int N>
+__device__ __forceinline__ void vm_wait() {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
 
 // DELTA: the increment form (as k_tb3's): B = d^{m-1}; layer l keeps d_l = d_{l-1} + coef lap U_{l-1}
 // (d_{-1} = B, U_{-1} = A) and U_l = U_{l-1} + d_l; d is pointwise, so it rides in registers from
 // one layer to the next (same plane, next iteration) and never in LDS. The sweep stores d and U of
 // its last layer (O[0] = the next sweep's B, O[1] its A), with the last layer's self-wrap ranges.
-template <class T, int D, bool FIRST, int R, int NW, bool FM, int DEEP, bool DELTA = false>
+template <class T, int D, bool FIRST, int R, int NW, bool FM, bool DELTA = false>
 __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(1, 8))) k_tbn(const TbnParams<T> p) {
-    constexpr bool ADEEP = DEEP & 1;      // A(i+3) into the slot of A(i-1) (read from LDS)
-    constexpr int NB = DEEP & 2 ? 4 : 2;  // B slots: B(i + NB/2) prefetched at iteration i
-    constexpr int ADIST = ADEEP ? 3 : 2, BDIST = NB / 2;
     constexpr int TJ = NW * R;
-    using Gm = TbnGeom<D, TJ>;
+    constexpr int ES = sizeof(T);
+    using Gm = TbnGeom<D, TJ, ES, NW>;
     constexpr int NT = NW * 64;
-    constexpr int RP = (Gm::nall + NT - 1) / NT;  // ring positions per thread
-    constexpr unsigned ES = sizeof(T);
-    constexpr int NU = D - 1;                // own history: U_0 .. U_{D-2}
-    constexpr int NRU = D >= 3 ? D - 2 : 1;  // ring history: U_0 .. U_{D-3}
-    // Every staged (layer, buffer) tile is its own __shared__ object: distinct objects cannot
-    // alias, so the compiler may hoist a layer's LDS reads above the previous layer's LDS
-    // writes (other tiles) instead of issuing read -> wait -> compute -> write one layer at a
-    // time (one array with computed offsets serialised them, W3D_TBN_ONE_LDS). fp32 runs faster
-    // with the one array (W3D_TBN_ONE_LDS = 2, the default: fp64 objects, fp32 one array)
-    constexpr bool ONE = W3D_TBN_ONE_LDS == 1 || (W3D_TBN_ONE_LDS == 2 && sizeof(T) == 4);
+    constexpr int RP = (Gm::ncomp + NT - 1) / NT;  // computed ring positions per thread
+    constexpr int NU = D - 1;                      // own history: U_0 .. U_{D-2}
+    constexpr int NRU = D >= 3 ? D - 2 : 1;        // ring history: U_0 .. U_{D-3}
+    constexpr int W0 = Gm::W(0);
+    // Staged tiles: fp64 one __shared__ object per (layer, buffer) / DMA slot — distinct objects
+    // cannot alias, so the compiler may hoist a layer's LDS reads above the previous layer's
+    // writes; fp32 one array (measured faster there, profiles/deep_sweeps_r4.txt batches 21/30)
+    constexpr bool ONE = sizeof(T) == 4;
     __shared__ T lds[ONE ? Gm::total : 1];
-    constexpr int Z0 = Gm::size(0), Z1 = Gm::size(1), Z2 = Gm::size(D > 2 ? 2 : 1), Z3 = Gm::size(D > 3 ? 3 : 1);
-    constexpr int Y0 = ONE ? 1 : Z0, Y1 = ONE ? 1 : Z1, Y2 = ONE || D <= 2 ? 1 : Z2, Y3 = ONE || D <= 3 ? 1 : Z3;
-    __shared__ T t00[Y0], t01[Y0], t10[Y1], t11[Y1], t20[Y2], t21[Y2], t30[Y3], t31[Y3];
-    // staged layer s, buffer h, offset o in its frame
-    auto Lo = [&](auto sc, auto hc, int o) -> T& {
-        constexpr int s = decltype(sc)::value, h = decltype(hc)::value;
-        if constexpr (ONE) return lds[Gm::off(s) + h * Gm::size(s) + o];
-        else if constexpr (s == 0) return h ? t01[o] : t00[o];
-        else if constexpr (s == 1) return h ? t11[o] : t10[o];
-        else if constexpr (s == 2) return h ? t21[o] : t20[o];
-        else return h ? t31[o] : t30[o];
+    constexpr int ZA = ONE ? 1 : Gm::scells, ZB = ONE ? 1 : Gm::scells, Z1 = ONE ? 1 : Gm::cells(1);
+    constexpr int Z2 = ONE || D <= 2 ? 1 : Gm::cells(2), Z3 = ONE || D <= 3 ? 1 : Gm::cells(3);
+    __shared__ T tA0[ZA], tA1[ZA], tA2[ZA], tA3[ZA], tB0[ZB], tB1[ZB];
+    __shared__ T t10[Z1], t11[Z1], t20[Z2], t21[Z2], t30[Z3], t31[Z3];
+    // A slot q / B slot q (A-frame offsets) / U_{s-1} frame s, buffer h
+    auto Ap = [&](auto qc) -> T* {
+        constexpr int q = decltype(qc)::value;
+        if constexpr (ONE) return lds + Gm::a_off(q);
+        else if constexpr (q == 0) return tA0;
+        else if constexpr (q == 1) return tA1;
+        else if constexpr (q == 2) return tA2;
+        else return tA3;
     };
-    // ... at A-frame coordinates (y, x)
-    auto L = [&](auto sc, auto hc, int y, int x) -> T& { return Lo(sc, hc, Gm::at(decltype(sc)::value, y, x)); };
+    auto Bp = [&](auto qc) -> T* {
+        constexpr int q = decltype(qc)::value;
+        if constexpr (ONE) return lds + Gm::b_off(q);
+        else if constexpr (q == 0) return tB0;
+        else return tB1;
+    };
+    auto Up = [&](auto sc, auto hc) -> T* {
+        constexpr int s = decltype(sc)::value, h = decltype(hc)::value;
+        if constexpr (ONE) return lds + Gm::u_off(s, h);
+        else if constexpr (s == 1) return h ? t11 : t10;
+        else if constexpr (s == 2) return h ? t21 : t20;
+        else return h ? t31 : t30;
+    };
 
     const int bid = blockIdx.x;
     const int b = find_box(p, bid);
@@ -238,7 +319,7 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(1,
 
     // ---- own nodes ------------------------------------------------------------------------
     const int k = kb + lane;
-    unsigned oa[R], ob[R], os[R];
+    unsigned oa[R], os[R];  // seam-partner loads (ALIAS body), stores
     bool ovalid[R], ocd[R];
 #pragma unroll
     for (int r = 0; r < R; ++r) {
@@ -246,7 +327,6 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(1,
         ocd[r] = incd(j, k);
         ovalid[r] = k >= Bx.k0 && k <= Bx.k1 && j <= Bx.j1;
         oa[r] = boff(j, k, inb(j, k));
-        ob[r] = boff(j, k, !FIRST && inb(j, k) && ocd[r]);
         os[r] = boff(j, k, ovalid[r]);
     }
     const T otz = (k >= Bx.k0 && k <= Bx.k1) ? p.tz[k] : T(0);
@@ -263,10 +343,10 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(1,
         if (p.w_lo[1][g] <= ie && p.w_hi[1][g] >= ib) rare |= 2;
     }
     rare = __builtin_amdgcn_readfirstlane(rare);
-    // steady-state window [flo, fhi]: every layer on an own-range plane, prefetch live, off the
-    // periodic seam and the self-wrap planes (those sit at the ends of the x range, so each one
-    // trims the window from its nearer end)
-    int flo = ib + D - 1, fhi = min(ie + D - ADIST, ie + D - 1 - BDIST);
+    // steady-state window [flo, fhi]: every layer on an own-range plane, A(i+2) / B(i+1) still
+    // inside the work item, off the periodic seam and the self-wrap planes (those sit at the
+    // ends of the x range, so each one trims the window from its nearer end)
+    int flo = ib + D - 1, fhi = ie + D - 2;
     auto cut = [&](int lo, int hi) {
         if (lo > hi || hi < flo || lo > fhi) return;
         if (lo - flo <= fhi - hi) flo = hi + 1;
@@ -296,106 +376,75 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(1,
         else if (idx < 2 * wd + hd) rj = jt - d + c + (idx - 2 * wd), rk = kb - d;
         else rj = jt - d + c + (idx - 2 * wd - hd), rk = kb + kTK - 1 + d;
     };
-    int rg[RP], ry[RP], rx[RP];       // ring (0: none) and A-frame coordinates
-    unsigned ra_off[RP], rb_off[RP];  // A / B load offsets (kOOB when masked)
-    bool rcd[RP];                     // stencil-valued node (else 0: Dirichlet face)
+    int rg[RP], ro0[RP];  // ring (0: none) and A-frame offset
+    unsigned ra_off[RP];  // seam-partner load offsets (kOOB when masked)
+    bool rcd[RP];         // stencil-valued node (else 0: Dirichlet face)
+    int ry[RP], rx[RP];
 #pragma unroll
     for (int s = 0; s < RP; ++s) {
         const int q = threadIdx.x + s * NT;
         int g = 0, rj = jt, rk = kb;
 #pragma unroll
-        for (int d = 1; d <= D; ++d)
+        for (int d = 1; d < D; ++d)
             if (g == 0 && q < Gm::first(d + 1)) {
                 g = d;
-                const int idx = q - Gm::first(d);
-                if (d < D) {
-                    ring(d, d == D - 1 ? 1 : 0, idx, rj, rk);
-                } else if (idx < 4) {  // corner of ring D-1
-                    rj = (idx & 1) ? jt + TJ - 1 + (D - 1) : jt - (D - 1);
-                    rk = (idx & 2) ? kb + kTK - 1 + (D - 1) : kb - (D - 1);
-                } else {
-                    ring(D, 1, idx - 4, rj, rk);
-                }
+                ring(d, d == D - 1 ? 1 : 0, q - Gm::first(d), rj, rk);
             }
         rg[s] = g;
         ry[s] = rj - jt + D, rx[s] = rk - kb + D;
-        rcd[s] = g != 0 && g < D && incd(rj, rk);
+        ro0[s] = Gm::at(0, ry[s], rx[s]);
+        rcd[s] = g != 0 && incd(rj, rk);
         ra_off[s] = boff(rj, rk, g != 0 && inb(rj, rk));
-        rb_off[s] = boff(rj, rk, !FIRST && rcd[s] && inb(rj, rk));
-    }
-    // Predicated ring (W3D_TBN_RINGPRED=1, off: measured 1.6 % slower): every lane of a ring slot
-    // runs every ring layer its slot can hold, without a branch, so one plane body is one basic
-    // block; lanes whose ring does not evaluate layer l read the tile's first own node and write
-    // the trash cell after the tile, staging-only lanes with no ring likewise.
-    int sto[RP], rdo[RP][D - 1], wro[RP][D - 1];
-    sfor<RP>([&](auto sc) {
-        constexpr int s = decltype(sc)::value;
-        sto[s] = rg[s] ? Gm::at(0, ry[s], rx[s]) : Gm::cells(0);
-        sfor<D - 1>([&](auto lc) {
-            constexpr int l = decltype(lc)::value;
-            const bool act = rg[s] >= 1 && rg[s] <= D - 1 - l;
-            rdo[s][l] = act ? Gm::at(l, ry[s], rx[s]) : Gm::at(l, D, D);
-            wro[s][l] = act ? Gm::at(l + 1, ry[s], rx[s]) : Gm::cells(l + 1);
-        });
-    });
-
-    // slots (iteration i = i0 + q, phase P = q & 3): A(x) (x - i0 + 1) & 3 -> A(i-1) = P,
-    // A(i) = P+1, A(i+1) = P+2, A(i+2) = P+3; B(x) (x - i0) & 1; U_l(x) (x + l - i0) & 3 ->
-    // U_l of this iteration in P, of the last in P+3, of the one before in P+2
-    T a[4][R], bb[NB][R], u[NU][4][R];
-    T ra[RP][4], rb[RP][NB], ru[RP][NRU][4];
-    {
-        const auto rAm = prs(p.A, i0 - 1, pbytes), rA0 = prs(p.A, i0, pbytes), rA1 = prs(p.A, i0 + 1, pbytes);
-        const auto rA2 = prs(p.A, i0 + 2, ADEEP ? pbytes : 0u);  // ADEEP: A(i0+2) in the prologue too
-        const auto rB = prs(p.B, i0, pbytes), rB1 = prs(p.B, i0 + 1, NB == 4 ? pbytes : 0u);
-#pragma unroll
-        for (int r = 0; r < R; ++r) {
-            a[0][r] = bld<T>(rAm, oa[r]);
-            a[1][r] = bld<T>(rA0, oa[r]);
-            a[2][r] = bld<T>(rA1, oa[r]);
-            a[3][r] = ADEEP ? bld<T>(rA2, oa[r]) : T(0);
-            bb[0][r] = bld<T>(rB, ob[r]);
-#pragma unroll
-            for (int t = 1; t < NB; ++t) bb[t][r] = t == 1 && NB == 4 ? bld<T>(rB1, ob[r]) : T(0);
-#pragma unroll
-            for (int l = 0; l < NU; ++l)
-#pragma unroll
-                for (int t = 0; t < 4; ++t) u[l][t][r] = T(0);
-        }
-#pragma unroll
-        for (int s = 0; s < RP; ++s) {
-            ra[s][0] = bld<T>(rAm, ra_off[s]);
-            ra[s][1] = bld<T>(rA0, ra_off[s]);
-            ra[s][2] = bld<T>(rA1, ra_off[s]);
-            ra[s][3] = ADEEP ? bld<T>(rA2, ra_off[s]) : T(0);
-            rb[s][0] = bld<T>(rB, rb_off[s]);
-#pragma unroll
-            for (int t = 1; t < NB; ++t) rb[s][t] = t == 1 && NB == 4 ? bld<T>(rB1, rb_off[s]) : T(0);
-#pragma unroll
-            for (int l = 0; l < NRU; ++l)
-#pragma unroll
-                for (int t = 0; t < 4; ++t) ru[s][l][t] = T(0);
-        }
-        if constexpr (ADEEP) {  // A(i0-1) is read from the tile "staged last iteration" (buffer 1)
-#pragma unroll
-            for (int r = 0; r < R; ++r) L(Ic<0>{}, Ic<1>{}, D + w * R + r, D + lane) = a[0][r];
-#pragma unroll
-            for (int s = 0; s < RP; ++s)
-                if (rg[s]) L(Ic<0>{}, Ic<1>{}, ry[s], rx[s]) = ra[s][0];
-        }
     }
 
-    // Dirichlet-face masks of the computed values: a select (two v_cndmask per double) or, with
-    // W3D_TBN_MASKMUL, a product with a 0/1 register (one op; a face value may become -0)
+    // ---- LDS-DMA staging of A and B -------------------------------------------------------
+    // wave w fills slot rows w*RPW .. w*RPW + RPW-1 of A and B alike (rows past the frame are
+    // loaded and never read). Frame rows past the storage read 0 (past the plane's num_records)
+    // and frame columns past it the finite row padding / next row: both only ever feed nodes
+    // outside the stencil-valued region (masked to 0).
+    static_assert(Gm::RPW == 3, "dma_fill3: three slot rows per wave");
+    const unsigned sjb = unsigned(sj) * ES;
+    const unsigned src0 = unsigned((jt - D + w * Gm::RPW) * sj + kb - D + p.poff) * ES;
+    const unsigned lds0 = unsigned(w * Gm::RPW * W0 * ES);
+    auto fillA = [&](auto qc, int plane, bool live) {
+        dma_fill3<ES, W0 * ES, Gm::rowb>(prs(p.A, plane, live ? pbytes : 0u), src0, sjb, lds_addr(Ap(qc)), lds0);
+    };
+    auto fillB = [&](auto qc, int plane, bool live) {
+        dma_fill3<ES, W0 * ES, Gm::rowb>(prs(p.B, plane, live ? pbytes : 0u), src0, sjb, lds_addr(Bp(qc)), lds0);
+    };
+    // VM operations a steady plane issues after its DMA pieces: the stores of its last two layers
+    constexpr int NST = 2 * R;
+    // prologue: A(i0-1), A(i0), A(i0+1) into slots 0..2 (A(x) in slot (x - i0 + 1) & 3), B(i0)
+    // into slot 0 (B(x) in slot (x - i0) & 1)
+    fillA(Ic<0>{}, i0 - 1, true);
+    fillA(Ic<1>{}, i0, true);
+    fillA(Ic<2>{}, i0 + 1, true);
+    if constexpr (!FIRST) fillB(Ic<0>{}, i0, true);
+
+    // slots (iteration i = i0 + q, phase P = q & 3): U_l(x) (x + l - i0) & 3 -> U_l of this
+    // iteration in P, of the last in P+3, of the one before in P+2
+    T u[NU][4][R];
+    T ru[RP][NRU][4];
+#pragma unroll
+    for (int l = 0; l < NU; ++l)
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+            for (int r = 0; r < R; ++r) u[l][t][r] = T(0);
+#pragma unroll
+    for (int s = 0; s < RP; ++s)
+#pragma unroll
+        for (int l = 0; l < NRU; ++l)
+#pragma unroll
+            for (int t = 0; t < 4; ++t) ru[s][l][t] = T(0);
+
+    // Dirichlet-face masks of the computed values: a product with a 0/1 register (one op; a
+    // face value may become -0)
     T ocm[R], rcm[RP];
 #pragma unroll
     for (int r = 0; r < R; ++r) ocm[r] = ocd[r] ? T(1) : T(0);
 #pragma unroll
     for (int s = 0; s < RP; ++s) rcm[s] = rcd[s] ? T(1) : T(0);
-    auto cmask = [&](bool keep, T m, T v) {
-        if constexpr (W3D_TBN_MASKMUL) return v * m;
-        else return keep ? v : T(0);
-    };
     // increment form: d_l of the own rows / ring slots in a plane-parity slot (written at
     // iteration i for plane i - l, read by layer l+1 at iteration i+1: the same plane)
     constexpr int ND = DELTA ? D - 1 : 1, NRD = DELTA && D >= 3 ? D - 2 : 1;
@@ -415,9 +464,9 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(1,
 #pragma unroll
     for (int l = 0; l < D; ++l) ma[l] = T(kErrInit), chk[l] = T(0);
 
-    // layer-l arithmetic: lap() = Laplacian (exact) or coef*Laplacian (FM); upd() = the
-    // Taylor start (layer 0 of the first sweep) or the leapfrog from it
-    // FM: lap() defers the stencil (FmLap); the leapfrog takes it whole (stencil_math leap_fm)
+    // layer-l arithmetic: lap() = Laplacian (exact) or the deferred coef*Laplacian (FM, FmLap:
+    // the leapfrog takes it whole, stencil_math leap_fm); upd() = the Taylor start (layer 0 of
+    // the first sweep) or the leapfrog from it
     const T kc1 = FM ? fm_kc(p.fc[1][0], p.fc[1][1], p.fc[1][2]) : T(0);
     auto lap = [&](auto lc, T ctr, T xm, T xp, T ym, T yp, T zm, T zp) {
         constexpr int l = decltype(lc)::value;
@@ -481,96 +530,78 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(1,
         constexpr bool FAST = !ALIAS;
         constexpr int S0 = P & 3, S1 = (P + 1) & 3, S2 = (P + 2) & 3, S3 = (P + 3) & 3;
         constexpr int H0 = P & 1, H1 = (P + 1) & 1;
-        constexpr int SA = ADEEP ? S0 : S3;                           // slot of the A prefetch
-        constexpr int BC = P & (NB - 1), BP = (P + BDIST) & (NB - 1);  // B(i), B prefetch slots
+        // A(i-1) .. A(i+2) in A slots S0 .. S3, B(i) / B(i+1) in B slots H0 / H1
 
-        // ---- prefetch A(i+ADIST), B(i+BDIST) (own and ring; 0-record descriptors when done) --
-        constexpr int PRIO = W3D_TBN_PRIO >= 0 ? W3D_TBN_PRIO : (sizeof(T) == 4 ? 1 : 0);
-        if constexpr (PRIO) __builtin_amdgcn_s_setprio(PRIO);
-        {
-            const bool moreA = FAST || i + ADIST <= ie + D, moreB = FAST || i + BDIST <= ie + D - 1;
-            // timing ablation W3D_TBN_ABL bit 0: the steady loads pinned to plane ib (wrong values)
-            const int ia = (W3D_TBN_ABL & 1) ? ib : i + (moreA ? ADIST : 0), ibn = (W3D_TBN_ABL & 1) ? ib : i + (moreB ? BDIST : 0);
-            const auto rAn = prs(p.A, ia, moreA ? pbytes : 0u);
-            const auto rBn = prs(p.B, ibn, moreB ? pbytes : 0u);
-            // ADEEP: A(i-1) of the own nodes is read from LDS below; the ring's too
-#pragma unroll
-            for (int r = 0; r < R; ++r) {
-                a[SA][r] = bld<T>(rAn, oa[r]);
-                bb[BP][r] = bld<T>(rBn, ob[r]);
-            }
-#pragma unroll
-            for (int s = 0; s < RP; ++s) {
-                ra[s][SA] = bld<T>(rAn, ra_off[s]);
-                rb[s][BP] = bld<T>(rBn, rb_off[s]);
-            }
-        }
-        // ---- stage A(i) --------------------------------------------------------------------
-#pragma unroll
-        for (int r = 0; r < R; ++r) L(Ic<0>{}, Ic<H0>{}, D + w * R + r, D + lane) = a[S1][r];
-#pragma unroll
-        for (int s = 0; s < RP; ++s)
-            if constexpr (W3D_TBN_RINGPRED) Lo(Ic<0>{}, Ic<H0>{}, sto[s]) = ra[s][S1];
-            else if (rg[s]) L(Ic<0>{}, Ic<H0>{}, ry[s], rx[s]) = ra[s][S1];
-        if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
+        // ---- A(i+1), B(i) landed (issued one iteration ago: everything but the stores that
+        // followed them; the checked body waits for all) -> barrier -> DMA B(i+1), A(i+2) into
+        // the slots of B(i-1), A(i-2), whose last readers passed the barrier
+        if constexpr (FAST) vm_wait<NST>();
+        else vm_wait<0>();
         __syncthreads();
+        if constexpr (!FIRST) fillB(Ic<H1>{}, i + 1, FAST || i + 1 <= ie + D - 1);
+        fillA(Ic<S3>{}, i + 2, FAST || i + 2 <= ie + D);
 
         T ev[R];  // U_{D-1}(i - D + 1): stored and its errors taken below
 #pragma unroll
         for (int r = 0; r < R; ++r) ev[r] = T(0);
-        // W3D_TBN_GATHER: the LDS neighbours of a layer (own rows: the outer j neighbour and both
-        // k neighbours; ring slots: all four) are read before any of its writes — one LDS round
-        // trip per layer instead of one per row and ring slot (the compiler cannot move a read
-        // above a possibly aliasing write); 2: the next layer's reads also go ahead of this
-        // layer's arithmetic (they read other tiles than it writes)
-        T gown[2][R][4], gring[2][RP][4];
-        auto gather = [&](auto lc) {
-            constexpr int l = decltype(lc)::value, G = l & 1;
-            constexpr int HS = l == 0 ? H0 : H1;
+        // staged layer l at frame offset o: A(i) for layer 0, U_{l-1} of the last iteration else
+        auto St = [&](auto lc, int o) -> T {
+            constexpr int l = decltype(lc)::value;
+            if constexpr (l == 0) return Ap(Ic<S1>{})[o];
+            else return Up(lc, Ic<H1>{})[o];
+        };
+        sfor<D>([&](auto lc) {
+            constexpr int l = decltype(lc)::value;
+            constexpr int Wl = Gm::W(l);
+            const int x = i - l;
+            if (!(FAST || (x >= ib - (D - 1 - l) && x <= ie + (D - 1 - l)))) return;
+            // ---- a layer's LDS reads go ahead of its writes (one LDS round trip per layer; the
+            // compiler cannot move a read above a possibly aliasing write) ----
+            T gy[R][2], gz[R][2], gc[R], gxm[R], gxp[R], gpw[R];
 #pragma unroll
             for (int r = 0; r < R; ++r) {
                 const int y = D + w * R + r, xx = D + lane;
-                if (r == 0) gown[G][r][0] = L(lc, Ic<HS>{}, y - 1, xx);
-                if (r == R - 1) gown[G][r][1] = L(lc, Ic<HS>{}, y + 1, xx);
-                gown[G][r][2] = L(lc, Ic<HS>{}, y, xx - 1);
-                gown[G][r][3] = L(lc, Ic<HS>{}, y, xx + 1);
+                const int o = Gm::at(l, y, xx), oA = Gm::at(0, y, xx);
+                if (r == 0) gy[r][0] = St(lc, o - Wl);
+                if (r == R - 1) gy[r][1] = St(lc, o + Wl);
+                gz[r][0] = St(lc, o - 1), gz[r][1] = St(lc, o + 1);
+                if constexpr (l == 0) {
+                    gc[r] = Ap(Ic<S1>{})[oA], gxm[r] = Ap(Ic<S0>{})[oA], gxp[r] = Ap(Ic<S2>{})[oA];
+                    if constexpr (!FIRST) gpw[r] = Bp(Ic<H0>{})[oA];
+                } else if constexpr (l == 1 && !DELTA) {
+                    gpw[r] = Ap(Ic<S0>{})[oA];  // U_{-1} = A(i-1)
+                }
             }
+            T grn[RP][4], grc[RP], grxm[RP], grxp[RP], grpw[RP];
             if constexpr (l <= D - 2)
                 sfor<RP>([&](auto sc) {
                     constexpr int s = decltype(sc)::value;
                     if constexpr (Gm::ring_of(s * NT) <= D - 1 - l) {
-                        const int ro = W3D_TBN_RINGPRED ? rdo[s][l] : Gm::at(l, ry[s], rx[s]);
-                        constexpr int Wl = Gm::W(l);
-                        gring[G][s][0] = Lo(lc, Ic<HS>{}, ro - Wl);
-                        gring[G][s][1] = Lo(lc, Ic<HS>{}, ro + Wl);
-                        gring[G][s][2] = Lo(lc, Ic<HS>{}, ro - 1);
-                        gring[G][s][3] = Lo(lc, Ic<HS>{}, ro + 1);
+                        const int ro = Gm::at(l, ry[s], rx[s]);
+                        grn[s][0] = St(lc, ro - Wl), grn[s][1] = St(lc, ro + Wl);
+                        grn[s][2] = St(lc, ro - 1), grn[s][3] = St(lc, ro + 1);
+                        if constexpr (l == 0) {
+                            grc[s] = Ap(Ic<S1>{})[ro0[s]], grxm[s] = Ap(Ic<S0>{})[ro0[s]];
+                            grxp[s] = Ap(Ic<S2>{})[ro0[s]];
+                            if constexpr (!FIRST) grpw[s] = Bp(Ic<H0>{})[ro0[s]];
+                        } else if constexpr (l == 1 && !DELTA) {
+                            grpw[s] = Ap(Ic<S0>{})[ro0[s]];
+                        }
                     }
                 });
-        };
-        if constexpr (W3D_TBN_GATHER == 2) gather(Ic<0>{});
-        sfor<D>([&](auto lc) {
-            constexpr int l = decltype(lc)::value;
-            constexpr int HS = l == 0 ? H0 : H1;  // buffer of the staged layer read (A: this iteration)
-            constexpr int G = l & 1;
-            if constexpr (W3D_TBN_GATHER == 1) gather(lc);
-            if constexpr (W3D_TBN_GATHER == 2 && l + 1 < D) gather(Ic<l + 1>{});
-            const int x = i - l;
-            if (!(FAST || (x >= ib - (D - 1 - l) && x <= ie + (D - 1 - l)))) return;
             // ---- own nodes ----
             T v[R], dl[R];  // dl: the increment form's d of the last layer (stored to O[0])
 #pragma unroll
             for (int r = 0; r < R; ++r) {
                 const int y = D + w * R + r, xx = D + lane;
-                T ctr, xm, xp, pw;
-                // A(i-1): its register (ADEEP: taken by the prefetch) or the tile staged last iteration
-                auto am1 = [&]() { return ADEEP ? L(Ic<0>{}, Ic<H1>{}, y, xx) : a[S0][r]; };
+                T ctr, xm, xp, pw = T(0);
                 if constexpr (l == 0) {
-                    ctr = a[S1][r], xm = am1(), xp = a[S2][r], pw = bb[BC][r];
+                    ctr = gc[r], xm = gxm[r], xp = gxp[r];
+                    if constexpr (!FIRST) pw = gpw[r];
                 } else {
                     ctr = u[l - 1][S3][r], xp = u[l - 1][S0][r], xm = u[l - 1][S2][r];
-                    if constexpr (l == 1) pw = am1();
-                    else pw = u[l - 2][S2][r];
+                    if constexpr (l == 1 && !DELTA) pw = gpw[r];
+                    else if constexpr (l >= 2) pw = u[l - 2][S2][r];
                 }
                 if constexpr (ALIAS && l <= D - 2) {
                     if (x == p.an_i) xp = bld<T>(lrs(p.nP[l]), oa[r]);
@@ -578,30 +609,22 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(1,
                 }
                 // j neighbours inside the wave's R rows come from registers (the same values
                 // as the staged tile), only the outer two from LDS
-                auto ctr_of = [&](int q) { return l == 0 ? a[S1][q] : u[l > 0 ? l - 1 : 0][S3][q]; };
-                T ym, yp, zm, zp;
-                if constexpr (W3D_TBN_GATHER) {
-                    ym = r > 0 ? ctr_of(r - 1) : gown[G][r][0];
-                    yp = r < R - 1 ? ctr_of(r + 1) : gown[G][r][1];
-                    zm = gown[G][r][2], zp = gown[G][r][3];
-                } else {
-                    ym = r > 0 ? ctr_of(r - 1) : L(lc, Ic<HS>{}, y - 1, xx);
-                    yp = r < R - 1 ? ctr_of(r + 1) : L(lc, Ic<HS>{}, y + 1, xx);
-                    zm = L(lc, Ic<HS>{}, y, xx - 1), zp = L(lc, Ic<HS>{}, y, xx + 1);
-                }
-                const auto lp = lap(lc, ctr, xm, xp, ym, yp, zm, zp);
+                auto ctr_of = [&](int q) { return l == 0 ? gc[q] : u[l > 0 ? l - 1 : 0][S3][q]; };
+                const T ym = r > 0 ? ctr_of(r - 1) : gy[r][0];
+                const T yp = r < R - 1 ? ctr_of(r + 1) : gy[r][1];
+                const auto lp = lap(lc, ctr, xm, xp, ym, yp, gz[r][0], gz[r][1]);
                 if constexpr (DELTA) {
-                    const T dprev = l == 0 ? bb[BC][r] : dq[l > 0 ? l - 1 : 0][H1][r];
-                    const T dv = cmask(ocd[r], ocm[r], dnew(lc, dprev, lp));
-                    v[r] = cmask(ocd[r], ocm[r], ctr + dv);
+                    const T dprev = l == 0 ? pw : dq[l > 0 ? l - 1 : 0][H1][r];
+                    const T dv = dnew(lc, dprev, lp) * ocm[r];
+                    v[r] = (ctr + dv) * ocm[r];
                     if constexpr (l <= D - 2) dq[l][H0][r] = dv;
                     else dl[r] = dv;
                 } else {
-                    v[r] = cmask(ocd[r], ocm[r], upd(lc, ctr, pw, lp));
+                    v[r] = upd(lc, ctr, pw, lp) * ocm[r];
                 }
                 if constexpr (l <= D - 2) {
                     u[l][S0][r] = v[r];
-                    L(Ic<l + 1>{}, Ic<H0>{}, y, xx) = v[r];
+                    Up(Ic<l + 1>{}, Ic<H0>{})[Gm::at(l + 1, y, xx)] = v[r];
                 }
             }
             // ---- ring nodes (rings 1 .. D-1-l) ----
@@ -609,39 +632,32 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(1,
                 sfor<RP>([&](auto sc) {
                     constexpr int s = decltype(sc)::value;
                     if constexpr (Gm::ring_of(s * NT) <= D - 1 - l) {
-                        if (W3D_TBN_RINGPRED || (rg[s] >= 1 && rg[s] <= D - 1 - l)) {
-                            T ctr, xm, xp, pw;
-                            auto am1 = [&]() { return ADEEP ? L(Ic<0>{}, Ic<H1>{}, ry[s], rx[s]) : ra[s][S0]; };
+                        if (rg[s] >= 1 && rg[s] <= D - 1 - l) {
+                            T ctr, xm, xp, pw = T(0);
                             if constexpr (l == 0) {
-                                ctr = ra[s][S1], xm = am1(), xp = ra[s][S2], pw = rb[s][BC];
+                                ctr = grc[s], xm = grxm[s], xp = grxp[s];
+                                if constexpr (!FIRST) pw = grpw[s];
                             } else {
                                 ctr = ru[s][l - 1][S3], xp = ru[s][l - 1][S0], xm = ru[s][l - 1][S2];
-                                if constexpr (l == 1) pw = am1();
-                                else pw = ru[s][l - 2][S2];
+                                if constexpr (l == 1 && !DELTA) pw = grpw[s];
+                                else if constexpr (l >= 2) pw = ru[s][l - 2][S2];
                             }
                             if constexpr (ALIAS) {
                                 if (x == p.an_i) xp = bld<T>(lrs(p.nP[l]), ra_off[s]);
                                 if (x == p.ap_i) xm = bld<T>(lrs(p.pP[l]), ra_off[s]);
                             }
-                            const int ro = W3D_TBN_RINGPRED ? rdo[s][l] : Gm::at(l, ry[s], rx[s]);
-                            const int wo = W3D_TBN_RINGPRED ? wro[s][l] : Gm::at(l + 1, ry[s], rx[s]);
-                            constexpr int Wl = Gm::W(l);
-                            const auto lp = W3D_TBN_GATHER
-                                                ? lap(lc, ctr, xm, xp, gring[G][s][0], gring[G][s][1], gring[G][s][2],
-                                                      gring[G][s][3])
-                                                : lap(lc, ctr, xm, xp, Lo(lc, Ic<HS>{}, ro - Wl), Lo(lc, Ic<HS>{}, ro + Wl),
-                                                      Lo(lc, Ic<HS>{}, ro - 1), Lo(lc, Ic<HS>{}, ro + 1));
+                            const auto lp = lap(lc, ctr, xm, xp, grn[s][0], grn[s][1], grn[s][2], grn[s][3]);
                             T cv;
                             if constexpr (DELTA) {
-                                const T dprev = l == 0 ? rb[s][BC] : rdq[s][l > 0 ? l - 1 : 0][H1];
-                                const T dv = cmask(rcd[s], rcm[s], dnew(lc, dprev, lp));
-                                cv = cmask(rcd[s], rcm[s], ctr + dv);
+                                const T dprev = l == 0 ? pw : rdq[s][l > 0 ? l - 1 : 0][H1];
+                                const T dv = dnew(lc, dprev, lp) * rcm[s];
+                                cv = (ctr + dv) * rcm[s];
                                 if constexpr (l <= D - 3) rdq[s][l][H0] = dv;
                             } else {
-                                cv = cmask(rcd[s], rcm[s], upd(lc, ctr, pw, lp));
+                                cv = upd(lc, ctr, pw, lp) * rcm[s];
                             }
                             if constexpr (l <= D - 3) ru[s][l][S0] = cv;
-                            Lo(Ic<l + 1>{}, Ic<H0>{}, wo) = cv;
+                            Up(Ic<l + 1>{}, Ic<H0>{})[Gm::at(l + 1, ry[s], rx[s])] = cv;
                         }
                     }
                 });
@@ -649,7 +665,7 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(1,
             // ---- stores of the last two layers (own planes, + periodic self-wrap); the increment
             // form stores d and U of the last layer (O[0] then has the last layer's wrap ranges) --
             auto put = [&](const int o, const T(&val)[R]) {
-                const auto rd = prs(p.O[o], (W3D_TBN_ABL & 2) ? ib : x, pbytes);  // ablation bit 1: stores pinned
+                const auto rd = prs(p.O[o], x, pbytes);
 #pragma unroll
                 for (int r = 0; r < R; ++r) bst<2>(val[r], rd, os[r]);
                 if (!FAST && (rare & (1 << o))) {
@@ -700,8 +716,7 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(1,
                 if constexpr (FM) {
 #pragma unroll
                     for (int r = 0; r < R; ++r) {
-                        if constexpr (W3D_TBN_MASKMUL) chk[l] = fma_t(val[r], om[r], chk[l]);
-                        else chk[l] += ovalid[r] ? val[r] : T(0);
+                        chk[l] = fma_t(val[r], om[r], chk[l]);
                         const T dv = (val[r] - fb[r] * p.ct[l]) * m[r];
                         ma[l] = max_abs(ma[l], dv);
                         mr[l].add(dv, wq[r]);
@@ -730,7 +745,7 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(1,
     // phase-0 plane of the steady window, the steady body over whole groups of 4 inside it, the
     // checked body for the rest. One loop choosing the body per plane kept every value of the
     // checked body live through the steady one: 337 SGPR spills and 249 VGPRs at D = 4, against
-    // none and 196 for the steady body alone.
+    // none and 196 for the steady body alone (round 4, register staging).
     const int iend = ie + D - 1;
     const int fstart = __builtin_amdgcn_readfirstlane(i0 + ((max(flo, i0) - i0 + 3) & ~3));
     // whole groups of 4 steady planes from fstart (none when the window is shorter)
@@ -754,14 +769,20 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(1,
 #pragma nounroll
     for (int pass = 0; pass < 2; ++pass) {
         checked(i, pass == 0 ? min(fstart, iend + 1) : iend + 1);
-        if (pass == 0 && i == fstart)  // (a work item shorter than the window start ran through)
+        if (pass == 0 && i == fstart) {  // (a work item shorter than the window start ran through)
+            // the steady body's counted wait assumes its predecessor issued NST operations
+            // after its DMA pieces; the checked body's may differ: drain them here
+            vm_wait<0>();
             for (; i < fend; i += 4) {
                 plane(Ph<0>{}, std::false_type{}, i);
                 plane(Ph<1>{}, std::false_type{}, i + 1);
                 plane(Ph<2>{}, std::false_type{}, i + 2);
                 plane(Ph<3>{}, std::false_type{}, i + 3);
             }
+        }
     }
+    // no DMA may still be writing this workgroup's LDS when it exits
+    vm_wait<0>();
     sfor<D>([&](auto lc) {
         constexpr int l = decltype(lc)::value;
         T rel;
@@ -772,69 +793,35 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(1,
     });
 }
 
-// load-pipeline variant (DEEP bits, see the top of the file): WAVE3D_TBN_DEEP, default kTbnDeep;
-// fp64 --math fma sweeps have all four, the others the default only
-constexpr int kTbnDeep = 0;
-int tbn_deep() {
-    static const int d = [] {
-        const char* e = std::getenv("WAVE3D_TBN_DEEP");
-        return e && *e ? std::atoi(e) & 3 : kTbnDeep;
-    }();
-    return d;
-}
-
 template <class T, int D, bool F>
-static void (*tbn_kernel(int rows, int waves, bool fm, int deep, bool delta))(const TbnParams<T>) {
-    // the increment form: fp32 at depth 4 (config 5's scheme; the fp64 one needs ~30 more VGPRs
-    // than the 248 of the leapfrog sweep has room for)
+static void (*tbn_kernel(int rows, int waves, bool fm, bool delta))(const TbnParams<T>) {
+    if (rows != 2 || waves != 8) return nullptr;
+    // the increment form: fp32 at depth 4 (config 5's scheme; fp64 uses the leapfrog)
     if (delta) {
         if constexpr (std::is_same_v<T, float> && D == 4)
-            if (deep == kTbnDeep && rows == 2 && waves == 8)
-                return fm ? k_tbn<T, D, F, 2, 8, true, kTbnDeep, true> : k_tbn<T, D, F, 2, 8, false, kTbnDeep, true>;
+            return fm ? k_tbn<T, D, F, 2, 8, true, true> : k_tbn<T, D, F, 2, 8, false, true>;
         return nullptr;
     }
-#ifdef W3D_TBN_ONLY  // codegen experiments: one instantiation (fp64, fma, not first, default DEEP)
-#ifndef W3D_TBN_PROBE_R
-#define W3D_TBN_PROBE_R 2
-#define W3D_TBN_PROBE_NW 8
-#endif
-    constexpr int PR = W3D_TBN_PROBE_R, PW = W3D_TBN_PROBE_NW;
-    if constexpr (std::is_same_v<T, double> && !F && D == W3D_TBN_ONLY)
-        return fm && deep == kTbnDeep && rows == PR && waves == PW ? k_tbn<T, D, F, PR, PW, true, kTbnDeep> : nullptr;
-    else return nullptr;
-#else
-#ifdef W3D_TBN_DEEP_VARIANTS  // load-pipeline A/B (fp64 --math fma): WAVE3D_TBN_DEEP = 0..3
-    if constexpr (std::is_same_v<T, double>)
-        if (fm && rows == 2 && waves == 8) switch (deep) {
-                case 0: return k_tbn<T, D, F, 2, 8, true, 0>;
-                case 1: return k_tbn<T, D, F, 2, 8, true, 1>;
-                case 2: return k_tbn<T, D, F, 2, 8, true, 2>;
-                case 3: return k_tbn<T, D, F, 2, 8, true, 3>;
-                default: return nullptr;
-            }
-#endif
-    if (deep != kTbnDeep) return nullptr;
-    if (rows == 2 && waves == 8) return fm ? k_tbn<T, D, F, 2, 8, true, kTbnDeep> : k_tbn<T, D, F, 2, 8, false, kTbnDeep>;
-    return nullptr;
-#endif
+    return fm ? k_tbn<T, D, F, 2, 8, true> : k_tbn<T, D, F, 2, 8, false>;
 }
 
 template <class T, bool F>
-static void (*tbn_kernel_d(int depth, int rows, int waves, bool fm, int deep, bool delta = false))(const TbnParams<T>) {
-    if (depth == 4) return tbn_kernel<T, 4, F>(rows, waves, fm, deep, delta);
+static void (*tbn_kernel_d(int depth, int rows, int waves, bool fm, bool delta = false))(const TbnParams<T>) {
+    if (depth == 4) return tbn_kernel<T, 4, F>(rows, waves, fm, delta);
     if constexpr (std::is_same_v<T, double>)  // depth 3: fp64 (the cross-check of k_tb3, A/B)
-        if (depth == 3) return tbn_kernel<T, 3, F>(rows, waves, fm, deep, delta);
+        if (depth == 3) return tbn_kernel<T, 3, F>(rows, waves, fm, delta);
     return nullptr;
 }
 
 }  // namespace
 
-bool tbn_supported(int depth, int rows, int waves, bool fm) {
-    return tbn_kernel_d<double, false>(depth, rows, waves, fm, kTbnDeep) != nullptr;
+bool tbn_supported(int depth, int rows, int waves, bool fm, bool fp32) {
+    return fp32 ? tbn_kernel_d<float, false>(depth, rows, waves, fm) != nullptr
+                : tbn_kernel_d<double, false>(depth, rows, waves, fm) != nullptr;
 }
 bool tbn_delta_supported(int depth, int rows, int waves, bool fm, bool fp32) {
-    return fp32 ? tbn_kernel_d<float, false>(depth, rows, waves, fm, kTbnDeep, true) != nullptr
-                : tbn_kernel_d<double, false>(depth, rows, waves, fm, kTbnDeep, true) != nullptr;
+    return fp32 ? tbn_kernel_d<float, false>(depth, rows, waves, fm, true) != nullptr
+                : tbn_kernel_d<double, false>(depth, rows, waves, fm, true) != nullptr;
 }
 
 template <class T>
@@ -847,11 +834,10 @@ void launch_tbn(int depth, int rows, int waves, bool fm, bool first, const T* A,
     W3D_REQUIRE(!fm || (txr && rtz), "tbn --math fma needs the reciprocal analytic tables");
     W3D_REQUIRE(gv.G >= depth, "deep temporal blocking needs ghost depth >= layers per sweep");
     W3D_REQUIRE(nbox >= 1 && nbox <= kMaxBoxes, "bad box count");
-    W3D_REQUIRE(gv.si * i64(sizeof(T)) < (i64(1) << 31), "tbn: plane larger than 2 GiB");
-    const int deep = tbn_deep();
-    auto kern = first ? tbn_kernel_d<T, true>(depth, rows, waves, fm, deep, delta)
-                      : tbn_kernel_d<T, false>(depth, rows, waves, fm, deep, delta);
-    W3D_REQUIRE(kern, "tbn: no instantiation of this depth x tile x dtype x math x scheme x WAVE3D_TBN_DEEP");
+    W3D_REQUIRE(gv.si * i64(sizeof(T)) < (i64(1) << 30), "tbn: plane larger than 1 GiB (LDS-DMA range marker)");
+    auto kern = first ? tbn_kernel_d<T, true>(depth, rows, waves, fm, delta)
+                      : tbn_kernel_d<T, false>(depth, rows, waves, fm, delta);
+    W3D_REQUIRE(kern, "tbn: no instantiation of this depth x tile x dtype x math x scheme");
     TbnParams<T> p{};
     p.pbytes = unsigned(gv.si * i64(sizeof(T)));
     p.pbias = gv.G + 1;  // plane indices reach ib - depth >= 1 - G and the wrap targets

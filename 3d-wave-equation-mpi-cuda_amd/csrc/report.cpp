@@ -98,7 +98,8 @@ std::string json_summary(const Config& c, const RunResult& r) {
       << "\", \"kernel\": \"" << r.kernel << "\", \"scheme\": \"" << r.scheme << "\", \"math\": \"" << r.math
       << "\", \"transport\": \"" << r.transport << "\""
       << ", \"overlap\": " << (r.overlap ? "true" : "false") << ", \"overlap_mode\": \"" << r.overlap_mode
-      << "\", \"overlap_order\": \"" << r.overlap_order << "\""
+      << "\", \"overlap_order\": \"" << r.overlap_order << "\", \"overlap_order_run\": \"" << r.overlap_order_run
+      << "\""
       << ", \"overlap_trial_ms\": [" << jnum(r.overlap_trial_ms[0]) << ", " << jnum(r.overlap_trial_ms[1]) << ", "
       << jnum(r.overlap_trial_ms[2]) << "]"
       << ", \"overlap_trials_ms\": [";

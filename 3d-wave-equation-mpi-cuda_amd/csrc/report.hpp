@@ -47,7 +47,8 @@ struct RunResult {
     // on with the shells first) and every trial in order (the three arms, twice)
     double overlap_trial_ms[3] = {0, 0, 0};
     double overlap_trials[kOverlapTrialSolves] = {};
-    std::string overlap_order = "beside";  // effective overlap order: beside | shells_first
+    std::string overlap_order = "none";  // effective overlap order: beside | shells_first | none
+    std::string overlap_order_run = "none";  // order of the enqueued (or replayed) layers
     int comm_size = 0;     // ranks the transport's communicator reports (ncclCommCount), 0 = none
     int rccl_max_ctas = -1;  // CTA budget of the RCCL communicator (0 = RCCL's own), -1 = none
     long rccl_mirror_msgs = 0;  // --rccl-mirror: messages sent through RCCL and compared

@@ -219,7 +219,7 @@ def tbn_sweep(A, B, O0, O1, boxes, *, depth: int, first: bool, cdom, err_i, tx, 
         boxes = [boxes]
     bl = [_check_box_g(b, gv) for b in boxes]
     ok = (_C().tbn_delta_supported(int(depth), int(rows), int(waves), bool(fma), A.dtype == torch.float32)
-          if delta else _C().tbn_supported(int(depth), int(rows), int(waves), bool(fma)))
+          if delta else _C().tbn_supported(int(depth), int(rows), int(waves), bool(fma), A.dtype == torch.float32))
     if not ok:
         raise ValueError(f"unsupported depth={depth} tile rows={rows} waves={waves} fma={fma} delta={delta}")
     if len(coefs) != depth or len(errs) != depth:

@@ -292,6 +292,10 @@ def main() -> int:
                 out["linf_vs_fp64"] = round(out["linf_abs"] / r64.linf_abs, 3) if r64.linf_abs > 0 else None
             del s64
         except Exception as e:  # noqa: BLE001 — the reference is an extra, never the result
+            # ... on one rank; with several, a rank that failed inside the solve would leave its
+            # peers waiting in the exchange until the launcher's timeout: fail the job at once
+            if world > 1:
+                raise
             out["linf_fp64_ref_skipped"] = f"reference solve failed: {e}"[:300]
         gc.collect()
     if rank == 0:

@@ -35,6 +35,11 @@ CASES = [
     ("2,2,2", "tb3", "fp64", 226, "direct"),   # alias A corner (-1,+1,-1)
     ("2,2,2", "tb3", "fp64", 227, "direct"),   # alias B corner (-1,+1,-1)
     ("4,1,1", "tb3r1w8", "fp64", 13, "direct"),   # x face planes of the B level
+    # the default leapfrog kernel (tb4: 4-deep A halos, 3-deep B halos, alias planes of A and B)
+    ("2,2,2", "tb4", "fp64", 296, "direct"),   # depth-4 corner (+1,+1,-1), level A
+    ("2,2,2", "tb4", "fp64", 227, "direct"),   # alias B corner (-1,+1,-1)
+    ("2,1,1", "tb4", "fp64", 24, "direct"),    # seam alias plane of B, to the last x-rank
+    ("1,2,2", "tb4", "fp32", 261, "direct"),   # y/z edge (0,+1,-1), level B, x ghosts by wrap
 ]
 
 
@@ -114,9 +119,24 @@ def test_overlap_auto_trials_then_keeps_the_faster(gpu_prog):
     assert r["overlap_mode"] == "auto" and len(trials) == 6 and min(trials) > 0
     assert on == min(trials[0], trials[3]) and off == min(trials[1], trials[4]) and first == min(trials[2], trials[5])
     best = min(on, off, first)  # ties keep the earlier arm
+    assert r["overlap_order_run"] == r["overlap_order"]
     if on == best:
         assert r["overlap"] and r["overlap_order"] == "beside"
     elif off == best:
         assert not r["overlap"]
     else:
         assert r["overlap"] and r["overlap_order"] == "shells_first"
+
+
+@pytest.mark.parametrize("graph", ["on", "auto"])
+def test_overlap_auto_graph_replays_the_reported_order(gpu_prog, graph):
+    """--overlap auto with captured graphs (--graph on): every change of arm — the overlap on/off
+    state or only the shell order — drops the captured graph, so the order that actually runs
+    (recorded when the layers are enqueued, i.e. at capture) is the order reported, at every
+    solve count through the trials and after them."""
+    for repeat in (3, 4, 7, 9):
+        out, _ = _run(gpu_prog, "2,1,1", "tb4", "fp64", ["--repeat", str(repeat), "--graph", graph])
+        assert out.returncode == 0, out.stderr[-2000:]
+        r = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][0])
+        assert r["overlap_mode"] == "auto"
+        assert r["overlap_order_run"] == r["overlap_order"], (repeat, r["overlap_order_run"], r["overlap_order"])

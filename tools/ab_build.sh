@@ -16,7 +16,9 @@ for v in "$@"; do
     out=../gpurun_ab/$name; mkdir -p $out
     vobjs=""
     for src in $srcs; do
-      $ROCM/bin/hipcc $FLAGS $extra -c csrc/$src.hip -o $out/$src.o
+      # the Makefile's per-object flags (NOSLP_OBJS), so a baseline arm builds the shipped code
+      obj_flags=$(make -s -n build/hip/$src.o -W csrc/$src.hip 2>/dev/null | grep -o -- '-fno-slp-vectorize -mllvm -amdgpu-sched-strategy=[a-z-]*' | head -1)
+      $ROCM/bin/hipcc $FLAGS $obj_flags $extra -c csrc/$src.hip -o $out/$src.o
       vobjs="$vobjs $out/$src.o"
     done
     $ROCM/bin/hipcc -shared --offload-arch=gfx950 $objs $vobjs -L$ROCM/lib -lamdhip64 -lrccl \
