@@ -50,6 +50,26 @@
 
 #include "device_common.hpp"
 
+// A/B: 1 = a layer's LDS reads issued before the previous layer's arithmetic (software
+// pipelining by one layer), 0 = after it
+#ifndef W3D_TBN_PIPE
+#define W3D_TBN_PIPE 0
+#endif
+#ifndef W3D_TBN_PIN  // A/B: 0 = ring reads not pinned (LLVM sinks them behind the own writes)
+#define W3D_TBN_PIN 1
+#endif
+// The gathers' LDS reads are volatile: LLVM neither sinks them into the ring branch nor pairs
+// them into ds_read2_b64, which moves 16 B per lane in 8 LDS cycles where two ds_read_b64 take 4
+// (MI355X LDS rates); 0 = plain reads (pinned ring values, compiler pairing)
+#ifndef W3D_TBN_VOL
+#define W3D_TBN_VOL 1
+#endif
+// A/B: where a plane issues its DMA pieces: 0 = right after the barrier, l + 1 = after layer
+// l's LDS reads (their landing then does not compete with the first read burst)
+#ifndef W3D_TBN_DMAPOS
+#define W3D_TBN_DMAPOS 0
+#endif
+
 namespace wave3d {
 namespace {
 
@@ -103,15 +123,13 @@ template <int D, int TJ, int ES, int NW>
 struct TbnGeom {
     // staged layer s: 0 = A (ring D), s >= 1 = U_{s-1} (ring D - s); frame origin (s, s)
     static constexpr int H(int s) { return TJ + 2 * (D - s); }
-    // row pitch of the U frames (ds_write): the staged width rounded up to odd, so the lanes of
-    // a ring column (one k, consecutive rows) hit 32 distinct ds_read_b64 bank pairs (an even
-    // pitch of 72 doubles put 8 rows on one pair: 4.6x the bank-conflict cycles of k_tb3 in the
-    // first tb4 PMC). The A / B slots (LDS-DMA) of fp64 take whole 16-B pieces per lane, so
-    // their pitch is even: 2 mod 4 doubles (20 r mod 64 banks: 16 distinct pairs, a 2-way
-    // conflict on 32-row column reads at most); fp32 slots keep the odd pitch (dword pieces).
-    static constexpr int W(int s) {
-        return s > 0 || ES != 8 ? (kTK + 2 * (D - s)) | 1 : (kTK + 2 * D) % 4 == 2 ? kTK + 2 * D : kTK + 2 * D + 2;
-    }
+    // row pitch: the staged width rounded up to odd, so the lanes of a ring column (one k,
+    // consecutive rows) hit 32 distinct ds_read_b64 bank pairs (an even pitch of 72 doubles put
+    // 8 rows on one pair: 4.6x the bank-conflict cycles of k_tb3 in the first tb4 PMC; 74 still
+    // 2-way: twice the conflict cycles of 73 in the LDS-DMA build). The fp64 A/B slots' rows are
+    // filled by 16-B DMA pieces from an 8-B-aligned LDS row start every other row: the gfx950
+    // LDS-DMA writes them in place (tools/microbench/lds_dma_probe.hip, case E).
+    static constexpr int W(int s) { return (kTK + 2 * (D - s)) | 1; }
     static constexpr int cells(int s) { return H(s) * W(s); }
     static constexpr int at(int s, int y, int x) { return (y - s) * W(s) + (x - s); }
     // A and B (= u^{m-2}, read by layer 0 on the tile + (D-1)-ring only) slots: the A frame
@@ -149,7 +167,7 @@ __device__ __forceinline__ unsigned lds_addr(T* ptr) {
 // lds_dma_probe.hip: the destination is M0 + instruction offset + size * lane, the source moves
 // by the instruction offset too, out-of-range lanes write 0, masked lanes nothing). Row q: source
 // src0 + q sjb (+ lane piece), LDS slot + lds0 + q ROWB.
-//   fp64: one buffer_load_dwordx4 per row (rowb / 16 lanes, 16 B each: the even slot pitch);
+//   fp64: one buffer_load_dwordx4 per row (rowb / 16 lanes, 16 B each);
 //   fp32: two buffer_load_dword per row (256 B, then the rowb - 256 B tail; odd pitch).
 // One asm statement per fill, so hipcc neither counts nor drains the pieces (vmcnt is ours:
 // vm_wait) and nothing per row is hoisted into SGPRs. M0 is written in the statement that reads
@@ -212,6 +230,18 @@ __device__ __forceinline__ void dma_fill3(__amdgpu_buffer_rsrc_t r, unsigned src
               [rs] "s"(r), [rowb] "i"(ROWB), [mask] "s"(u64((1ull << ((RB - 256) / 4)) - 1))
             : "memory", "scc");
     }
+}
+// LDS read of t[o] for the layer gathers (W3D_TBN_VOL)
+template <class T>
+__device__ __forceinline__ T ldsr(const T* t, int o) {
+    using LP = const volatile __attribute__((address_space(3))) T*;  // an LDS access, not flat
+    if constexpr (W3D_TBN_VOL) return ((LP)(t))[o];
+    else return t[o];
+}
+// x opaque at this point: its producer stays above (used here), its consumers below
+template <class T>
+__device__ __forceinline__ void pin(T& x) {
+    asm volatile("" : "+v"(x));
 }
 template <int N>
 __device__ __forceinline__ void vm_wait() {
@@ -538,8 +568,11 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(1,
         if constexpr (FAST) vm_wait<NST>();
         else vm_wait<0>();
         __syncthreads();
-        if constexpr (!FIRST) fillB(Ic<H1>{}, i + 1, FAST || i + 1 <= ie + D - 1);
-        fillA(Ic<S3>{}, i + 2, FAST || i + 2 <= ie + D);
+        auto fills = [&]() {
+            if constexpr (!FIRST) fillB(Ic<H1>{}, i + 1, FAST || i + 1 <= ie + D - 1);
+            fillA(Ic<S3>{}, i + 2, FAST || i + 2 <= ie + D);
+        };
+        if constexpr (W3D_TBN_DMAPOS == 0) fills();
 
         T ev[R];  // U_{D-1}(i - D + 1): stored and its errors taken below
 #pragma unroll
@@ -547,48 +580,97 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(1,
         // staged layer l at frame offset o: A(i) for layer 0, U_{l-1} of the last iteration else
         auto St = [&](auto lc, int o) -> T {
             constexpr int l = decltype(lc)::value;
-            if constexpr (l == 0) return Ap(Ic<S1>{})[o];
-            else return Up(lc, Ic<H1>{})[o];
+            if constexpr (l == 0) return ldsr(Ap(Ic<S1>{}), o);
+            else return ldsr(Up(lc, Ic<H1>{}), o);
         };
-        sfor<D>([&](auto lc) {
+        // ---- a layer's LDS reads, own nodes and ring together (one LDS round trip per layer):
+        // issued ahead of the previous layer's arithmetic and writes (they read the frames of
+        // the last iteration, other objects than this iteration's writes) and pinned — waited
+        // for — before the layer's own arithmetic (W3D_TBN_PIPE; 0: after the previous layer)
+        struct Gath {
+            T gy[R][2], gz[R][2], gc[R], gxm[R], gxp[R], gpw[R];
+            T grn[RP][4], grc[RP], grxm[RP], grxp[RP], grpw[RP];
+        };
+        Gath gt[2];
+        auto gather = [&](auto lc) {
             constexpr int l = decltype(lc)::value;
             constexpr int Wl = Gm::W(l);
-            const int x = i - l;
-            if (!(FAST || (x >= ib - (D - 1 - l) && x <= ie + (D - 1 - l)))) return;
-            // ---- a layer's LDS reads go ahead of its writes (one LDS round trip per layer; the
-            // compiler cannot move a read above a possibly aliasing write) ----
-            T gy[R][2], gz[R][2], gc[R], gxm[R], gxp[R], gpw[R];
+            Gath& g = gt[l & 1];
 #pragma unroll
             for (int r = 0; r < R; ++r) {
                 const int y = D + w * R + r, xx = D + lane;
                 const int o = Gm::at(l, y, xx), oA = Gm::at(0, y, xx);
-                if (r == 0) gy[r][0] = St(lc, o - Wl);
-                if (r == R - 1) gy[r][1] = St(lc, o + Wl);
-                gz[r][0] = St(lc, o - 1), gz[r][1] = St(lc, o + 1);
+                if (r == 0) g.gy[r][0] = St(lc, o - Wl);
+                if (r == R - 1) g.gy[r][1] = St(lc, o + Wl);
+                g.gz[r][0] = St(lc, o - 1), g.gz[r][1] = St(lc, o + 1);
                 if constexpr (l == 0) {
-                    gc[r] = Ap(Ic<S1>{})[oA], gxm[r] = Ap(Ic<S0>{})[oA], gxp[r] = Ap(Ic<S2>{})[oA];
-                    if constexpr (!FIRST) gpw[r] = Bp(Ic<H0>{})[oA];
+                    g.gc[r] = ldsr(Ap(Ic<S1>{}), oA), g.gxm[r] = ldsr(Ap(Ic<S0>{}), oA), g.gxp[r] = ldsr(Ap(Ic<S2>{}), oA);
+                    if constexpr (!FIRST) g.gpw[r] = ldsr(Bp(Ic<H0>{}), oA);
                 } else if constexpr (l == 1 && !DELTA) {
-                    gpw[r] = Ap(Ic<S0>{})[oA];  // U_{-1} = A(i-1)
+                    g.gpw[r] = ldsr(Ap(Ic<S0>{}), oA);  // U_{-1} = A(i-1)
                 }
             }
-            T grn[RP][4], grc[RP], grxm[RP], grxp[RP], grpw[RP];
             if constexpr (l <= D - 2)
                 sfor<RP>([&](auto sc) {
                     constexpr int s = decltype(sc)::value;
                     if constexpr (Gm::ring_of(s * NT) <= D - 1 - l) {
                         const int ro = Gm::at(l, ry[s], rx[s]);
-                        grn[s][0] = St(lc, ro - Wl), grn[s][1] = St(lc, ro + Wl);
-                        grn[s][2] = St(lc, ro - 1), grn[s][3] = St(lc, ro + 1);
+                        g.grn[s][0] = St(lc, ro - Wl), g.grn[s][1] = St(lc, ro + Wl);
+                        g.grn[s][2] = St(lc, ro - 1), g.grn[s][3] = St(lc, ro + 1);
                         if constexpr (l == 0) {
-                            grc[s] = Ap(Ic<S1>{})[ro0[s]], grxm[s] = Ap(Ic<S0>{})[ro0[s]];
-                            grxp[s] = Ap(Ic<S2>{})[ro0[s]];
-                            if constexpr (!FIRST) grpw[s] = Bp(Ic<H0>{})[ro0[s]];
+                            g.grc[s] = ldsr(Ap(Ic<S1>{}), ro0[s]), g.grxm[s] = ldsr(Ap(Ic<S0>{}), ro0[s]);
+                            g.grxp[s] = ldsr(Ap(Ic<S2>{}), ro0[s]);
+                            if constexpr (!FIRST) g.grpw[s] = ldsr(Bp(Ic<H0>{}), ro0[s]);
                         } else if constexpr (l == 1 && !DELTA) {
-                            grpw[s] = Ap(Ic<S0>{})[ro0[s]];
+                            g.grpw[s] = ldsr(Ap(Ic<S0>{}), ro0[s]);
                         }
                     }
                 });
+        };
+        // the ring values are consumed inside the ring branch: unpinned, LLVM sinks their loads
+        // into it, behind the own nodes' LDS writes (a second LDS round trip per layer)
+        auto pin_ring = [&](auto lc) {
+            constexpr int l = decltype(lc)::value;
+            Gath& g = gt[l & 1];
+            if constexpr (W3D_TBN_PIN && !W3D_TBN_VOL && l <= D - 2)
+                sfor<RP>([&](auto sc) {
+                    constexpr int s = decltype(sc)::value;
+                    if constexpr (Gm::ring_of(s * NT) <= D - 1 - l) {
+                        sfor<4>([&](auto nc) { pin(g.grn[s][decltype(nc)::value]); });
+                        if constexpr (l == 0) {
+                            pin(g.grc[s]), pin(g.grxm[s]), pin(g.grxp[s]);
+                            if constexpr (!FIRST) pin(g.grpw[s]);
+                        } else if constexpr (l == 1 && !DELTA) {
+                            pin(g.grpw[s]);
+                        }
+                    }
+                });
+        };
+        if constexpr (W3D_TBN_PIPE) gather(Ic<0>{}), pin_ring(Ic<0>{});  // layer 0: nothing to overlap
+        sfor<D>([&](auto lc) {
+            constexpr int l = decltype(lc)::value;
+            const int x = i - l;
+            if constexpr (W3D_TBN_PIPE) {
+                if constexpr (l + 1 < D) gather(Ic<l + 1>{});
+                if constexpr (l > 0) pin_ring(lc);
+            } else {
+                gather(lc), pin_ring(lc);
+                // the DMA pieces after this layer's LDS reads (W3D_TBN_DMAPOS = l + 1)
+                if constexpr (W3D_TBN_DMAPOS == l + 1) fills();
+            }
+            Gath& g = gt[l & 1];
+            auto& gy = g.gy;
+            auto& gz = g.gz;
+            auto& gc = g.gc;
+            auto& gxm = g.gxm;
+            auto& gxp = g.gxp;
+            auto& gpw = g.gpw;
+            auto& grn = g.grn;
+            auto& grc = g.grc;
+            auto& grxm = g.grxm;
+            auto& grxp = g.grxp;
+            auto& grpw = g.grpw;
+            if (!(FAST || (x >= ib - (D - 1 - l) && x <= ie + (D - 1 - l)))) return;
             // ---- own nodes ----
             T v[R], dl[R];  // dl: the increment form's d of the last layer (stored to O[0])
 #pragma unroll

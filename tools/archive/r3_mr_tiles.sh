@@ -1,6 +1,6 @@
 #!/bin/bash
 # Simulated multi-rank bench configs (one GPU, loopback halos) for a list of fp64 fma kernels,
-# overlap off: tools/r3_mr_tiles.sh tb3r1w8 tb3 ...
+# overlap off: tools/archive/r3_mr_tiles.sh tb3r1w8 tb3 ...
 cd "$(dirname "$0")/.."
 B=${BIN:-3d-wave-equation-mpi-cuda_amd/build/wave3d}
 for k in "$@"; do

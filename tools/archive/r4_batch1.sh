@@ -4,5 +4,5 @@ echo "abl rc=$?"
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/gputest_r4a.log 2>&1
 rc=$?; echo "pytest rc=$rc"; tail -5 gpurun_out/gputest_r4a.log
 [ $rc -eq 0 ] || exit $rc
-timeout -k 10 400 tools/r4_fp32_scheme.sh > gpurun_out/fp32_scheme_r4.log 2>&1; echo "fp32 rc=$?"
+timeout -k 10 400 tools/archive/r4_fp32_scheme.sh > gpurun_out/fp32_scheme_r4.log 2>&1; echo "fp32 rc=$?"
 cat gpurun_out/abl_mem.log gpurun_out/fp32_scheme_r4.log

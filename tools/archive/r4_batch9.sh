@@ -6,5 +6,5 @@ timeout -k 10 600 python -u -m pytest tests/test_gpu_solver.py tests/test_gpu_tb
 rc=$?; echo "pytest rc=$rc"; tail -5 gpurun_out/gputest_fused.log; [ $rc -eq 0 ] || exit $rc
 tools/r4_ab_multi.sh 2 main:tb4:0 g1:tb4:0 g2:tb4:0 nofuse:tb4:0 nopred:tb4:0 onelds:tb4:0 main:tb3:0 nofuse:tb3:0 || exit 1
 EXTRA="--math exact" tools/r4_ab_multi.sh 1 main:tb4:0 g1:tb4:0 g2:tb4:0 nopred:tb4:0 onelds:tb4:0 || exit 1
-timeout -k 10 700 tools/r4_batch7.sh > gpurun_out/overlap_cus.log 2>&1; rc=$?; cat gpurun_out/overlap_cus.log; [ $rc -eq 0 ] || exit $rc
-timeout -k 10 480 tools/r4_pmc2.sh > gpurun_out/pmc_r4b.log 2>&1; rc=$?; cat gpurun_out/pmc_r4b.log; exit $rc
+timeout -k 10 700 tools/archive/r4_batch7.sh > gpurun_out/overlap_cus.log 2>&1; rc=$?; cat gpurun_out/overlap_cus.log; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 480 tools/archive/r4_pmc2.sh > gpurun_out/pmc_r4b.log 2>&1; rc=$?; cat gpurun_out/pmc_r4b.log; exit $rc

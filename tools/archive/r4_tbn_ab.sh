@@ -1,7 +1,7 @@
 #!/bin/bash
 # A/B of the deep-sweep load pipelines (WAVE3D_TBN_DEEP: bit 0 = A three planes ahead with A(i-1)
 # from LDS, bit 1 = B two planes ahead) against k_tb3: N=512 fp64 K=100 --math fma, best of 5
-# solves, alternating rounds. tools/r4_tbn_ab.sh ROUNDS "kernel:deep ..."
+# solves, alternating rounds. tools/archive/r4_tbn_ab.sh ROUNDS "kernel:deep ..."
 cd "$(dirname "$0")/.."
 W=3d-wave-equation-mpi-cuda_amd/build/wave3d
 rounds=$1; shift

@@ -31,10 +31,14 @@ __global__ void probe(const float* g, float* out, unsigned nbytes, unsigned base
         // D: instruction offset 256 B: added to the source AND to the LDS address? at base + 192
         unsigned m3 = (unsigned)(uintptr_t)(lds + base_dw + 192);
         asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tbuffer_load_dword %0, %2, 0 offen offset:256 lds" ::"v"(lane * 4u), "s"(m3), "s"(r) : "memory");
+        // E: dwordx4 pieces (16 B per lane) to an LDS address that is 8 mod 16, at base + 330
+        //    (dwords): the 8-B-aligned destination an odd fp64 row pitch gives every other row
+        unsigned m4 = (unsigned)(uintptr_t)(lds + base_dw + 330);
+        asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %2, 0 offen lds" ::"v"(lane * 16u), "s"(m4), "s"(r) : "memory");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     __syncthreads();
-    for (int q = threadIdx.x; q < 384; q += blockDim.x) out[q] = lds[base_dw + q];
+    for (int q = threadIdx.x; q < 600; q += blockDim.x) out[q] = lds[base_dw + q];
 }
 
 int main() {
@@ -42,12 +46,12 @@ int main() {
     for (int q = 0; q < 1024; ++q) h[q] = 1000.0f + q;
     float *g, *o;
     hipMalloc(&g, sizeof h);
-    hipMalloc(&o, 384 * sizeof(float));
+    hipMalloc(&o, 600 * sizeof(float));
     hipMemcpy(g, h, sizeof h, hipMemcpyHostToDevice);
     int bad = 0;
     for (unsigned base : {0u, 16400u, 40000u}) {  // 0, ~64 KiB, ~156 KiB
         hipLaunchKernelGGL(probe, dim3(1), dim3(256), 0, 0, g, o, unsigned(sizeof h), base);
-        float r[384];
+        float r[600];
         hipMemcpy(r, o, sizeof r, hipMemcpyDeviceToHost);
         int inr = 0, oobz = 0, oobu = 0, mk = 0, mu = 0, c0 = 0, cu = 0;
         for (int q = 0; q < 32; ++q) inr += r[q] == 1000.0f + q;
@@ -57,6 +61,11 @@ int main() {
         for (int q = 0; q < 64; ++q) c0 += r[128 + q] == 0.0f, cu += r[128 + q] == -1.0f;
         int d_both = 0, d_src = 0;
         for (int q = 0; q < 64; ++q) d_both += r[192 + 64 + q] == 1064.0f + q, d_src += r[192 + q] == 1064.0f + q;
+        int x4 = 0;
+        for (int q = 0; q < 256; ++q) x4 += r[330 + q] == 1000.0f + q;
+        printf("dwordx4 to an 8-mod-16 LDS address: %d/256 dwords where expected, guard before %s after %s\n", x4,
+               r[329] == -1.0f ? "ok" : "CLOBBERED", r[586] == -1.0f ? "ok" : "CLOBBERED");
+        bad += x4 != 256;
         printf("offset:256 -> LDS+256 & src+256: %d/64, LDS+0 & src+256: %d/64\n", d_both, d_src);
         printf("base_dw=%u in-range ok %d/32 | oob lanes: zero %d untouched %d | masked: active ok %d/18 untouched %d/46 | "
                "0-record desc: zero %d untouched %d\n", base, inr, oobz, oobu, mk, mu, c0, cu);
