@@ -288,7 +288,8 @@ public:
         const int trial = overlap_auto_ && solves_ >= 1 && trials_done_ < kOverlapTrials ? trials_done_ : -1;
         ++solves_;
         if (trial >= 0) set_overlap(trial % 3 != 1, trial % 3 == 2);
-        res.overlap = overlap_;
+        res.overlap = overlap_;  // of this solve (an --overlap auto decision applies from the next)
+        res.overlap_order = !overlap_ ? "none" : shells_first_ ? "shells_first" : "beside";
         res.overlap_mode = !(ext_ || world_ > 1) ? "none"
                            : overlap_auto_       ? "auto"
                            : (overlap_ ? "on" : "off");
@@ -326,7 +327,6 @@ public:
         }
         for (int a = 0; a < 3; ++a) res.overlap_trial_ms[a] = best_trial(a);
         for (int q = 0; q < kOverlapTrials; ++q) res.overlap_trials[q] = trial_ms_[q];
-        res.overlap_order = !overlap_ ? "none" : shells_first_ ? "shells_first" : "beside";
         res.overlap_order_run = order_enqueued_;
         res.t = t;
         res.solve_ms.push_back(t.total_ms);

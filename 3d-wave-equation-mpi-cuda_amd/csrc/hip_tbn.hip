@@ -50,24 +50,10 @@
 
 #include "device_common.hpp"
 
-// A/B: 1 = a layer's LDS reads issued before the previous layer's arithmetic (software
-// pipelining by one layer), 0 = after it
-#ifndef W3D_TBN_PIPE
-#define W3D_TBN_PIPE 0
-#endif
-#ifndef W3D_TBN_PIN  // A/B: 0 = ring reads not pinned (LLVM sinks them behind the own writes)
-#define W3D_TBN_PIN 1
-#endif
-// The gathers' LDS reads are volatile: LLVM neither sinks them into the ring branch nor pairs
-// them into ds_read2_b64, which moves 16 B per lane in 8 LDS cycles where two ds_read_b64 take 4
-// (MI355X LDS rates); 0 = plain reads (pinned ring values, compiler pairing)
-#ifndef W3D_TBN_VOL
-#define W3D_TBN_VOL 1
-#endif
-// A/B: where a plane issues its DMA pieces: 0 = right after the barrier, l + 1 = after layer
-// l's LDS reads (their landing then does not compete with the first read burst)
-#ifndef W3D_TBN_DMAPOS
-#define W3D_TBN_DMAPOS 0
+// Timing ablation (wrong error tables): no error reduction in the planes (what the fused errors
+// cost: profiles/deep_sweeps_r5.txt)
+#ifndef W3D_TBN_ABL_ERR
+#define W3D_TBN_ABL_ERR 0
 #endif
 
 namespace wave3d {
@@ -132,16 +118,20 @@ struct TbnGeom {
     static constexpr int W(int s) { return (kTK + 2 * (D - s)) | 1; }
     static constexpr int cells(int s) { return H(s) * W(s); }
     static constexpr int at(int s, int y, int x) { return (y - s) * W(s) + (x - s); }
-    // A and B (= u^{m-2}, read by layer 0 on the tile + (D-1)-ring only) slots: the A frame
-    // rounded up to RPW rows per wave (the rows past the frame are loaded and never read)
+    // A slots: the A frame rounded up to RPW rows per wave (rows past the frame are loaded and
+    // never read). B (= u^{m-2}, read by layer 0 on the tile + (D-1)-ring only): the same rows,
+    // columns 1 .. 64+2D-2 of the A frame at the U_0 frame's pitch W(1): B(y, x) at y W(1) + x - 1
     static constexpr int RPW = (H(0) + NW - 1) / NW;
     static constexpr int scells = RPW * NW * W(0);
-    static constexpr int rowb = (kTK + 2 * D) * ES;  // bytes a row's DMA moves
-    // one-array layout (fp32): A slots 0..3, B slots 0..1, then U_{s-1} frames x 2 buffers
+    static constexpr int bcells = RPW * NW * W(1);
+    static constexpr int rowb = (kTK + 2 * D) * ES;         // bytes an A row's DMA moves
+    static constexpr int browb = (kTK + 2 * D - 2) * ES;    // ... a B row's
+    static constexpr int bat(int y, int x) { return y * W(1) + x - 1; }
+    // one-array layout (fp32): A slots 0..3, B slots 0..2, then U_{s-1} frames x 2 buffers
     static constexpr int a_off(int q) { return q * scells; }
-    static constexpr int b_off(int q) { return (4 + q) * scells; }
+    static constexpr int b_off(int q) { return 4 * scells + q * bcells; }
     static constexpr int u_off(int s, int h) {
-        return s == 1 ? b_off(2) + h * cells(1) : u_off(s - 1, 1) + cells(s - 1) + h * cells(s);
+        return s == 1 ? b_off(3) + h * cells(1) : u_off(s - 1, 1) + cells(s - 1) + h * cells(s);
     }
     static constexpr int total = u_off(D - 1, 1) + cells(D - 1);
     // computed positions of ring r: rings 1..D-2 whole, D-1 without corners
@@ -231,17 +221,16 @@ __device__ __forceinline__ void dma_fill3(__amdgpu_buffer_rsrc_t r, unsigned src
             : "memory", "scc");
     }
 }
-// LDS read of t[o] for the layer gathers (W3D_TBN_VOL)
+// LDS read of t[o] for the layer gathers: volatile, so LLVM neither sinks it into the branch
+// that consumes it (the ring nodes': behind the own nodes' LDS writes, a second LDS round trip
+// per layer) nor pairs two of them into a ds_read2_b64, which moves 16 B per lane in 8 LDS
+// cycles where two ds_read_b64 take 4 (MI355X LDS rates; 13 pairs per plane before: +3-4 %,
+// profiles/deep_sweeps_r5.txt). Through an LDS-address-space pointer: a volatile generic access
+// would be a flat load.
 template <class T>
 __device__ __forceinline__ T ldsr(const T* t, int o) {
-    using LP = const volatile __attribute__((address_space(3))) T*;  // an LDS access, not flat
-    if constexpr (W3D_TBN_VOL) return ((LP)(t))[o];
-    else return t[o];
-}
-// x opaque at this point: its producer stays above (used here), its consumers below
-template <class T>
-__device__ __forceinline__ void pin(T& x) {
-    asm volatile("" : "+v"(x));
+    using LP = const volatile __attribute__((address_space(3))) T*;
+    return ((LP)(t))[o];
 }
 template <int N>
 __device__ __forceinline__ void vm_wait() {
@@ -267,9 +256,9 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(1,
     // writes; fp32 one array (measured faster there, profiles/deep_sweeps_r4.txt batches 21/30)
     constexpr bool ONE = sizeof(T) == 4;
     __shared__ T lds[ONE ? Gm::total : 1];
-    constexpr int ZA = ONE ? 1 : Gm::scells, ZB = ONE ? 1 : Gm::scells, Z1 = ONE ? 1 : Gm::cells(1);
+    constexpr int ZA = ONE ? 1 : Gm::scells, ZB = ONE ? 1 : 3 * Gm::bcells, Z1 = ONE ? 1 : Gm::cells(1);
     constexpr int Z2 = ONE || D <= 2 ? 1 : Gm::cells(2), Z3 = ONE || D <= 3 ? 1 : Gm::cells(3);
-    __shared__ T tA0[ZA], tA1[ZA], tA2[ZA], tA3[ZA], tB0[ZB], tB1[ZB];
+    __shared__ T tA0[ZA], tA1[ZA], tA2[ZA], tA3[ZA], tB[ZB];
     __shared__ T t10[Z1], t11[Z1], t20[Z2], t21[Z2], t30[Z3], t31[Z3];
     // A slot q / B slot q (A-frame offsets) / U_{s-1} frame s, buffer h
     auto Ap = [&](auto qc) -> T* {
@@ -280,11 +269,10 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(1,
         else if constexpr (q == 2) return tA2;
         else return tA3;
     };
-    auto Bp = [&](auto qc) -> T* {
-        constexpr int q = decltype(qc)::value;
-        if constexpr (ONE) return lds + Gm::b_off(q);
-        else if constexpr (q == 0) return tB0;
-        else return tB1;
+    // B slot q (runtime: B(x) in slot (x - i0) mod 3)
+    auto Bp = [&](int q) -> T* {
+        if constexpr (ONE) return lds + Gm::b_off(0) + q * Gm::bcells;
+        else return tB + q * Gm::bcells;
     };
     auto Up = [&](auto sc, auto hc) -> T* {
         constexpr int s = decltype(sc)::value, h = decltype(hc)::value;
@@ -373,10 +361,10 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(1,
         if (p.w_lo[1][g] <= ie && p.w_hi[1][g] >= ib) rare |= 2;
     }
     rare = __builtin_amdgcn_readfirstlane(rare);
-    // steady-state window [flo, fhi]: every layer on an own-range plane, A(i+2) / B(i+1) still
+    // steady-state window [flo, fhi]: every layer on an own-range plane, A(i+3) / B(i+2) still
     // inside the work item, off the periodic seam and the self-wrap planes (those sit at the
     // ends of the x range, so each one trims the window from its nearer end)
-    int flo = ib + D - 1, fhi = ie + D - 2;
+    int flo = ib + D - 1, fhi = ie + D - 3;
     auto cut = [&](int lo, int hi) {
         if (lo > hi || hi < flo || lo > fhi) return;
         if (lo - flo <= fhi - hi) flo = hi + 1;
@@ -406,7 +394,7 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(1,
         else if (idx < 2 * wd + hd) rj = jt - d + c + (idx - 2 * wd), rk = kb - d;
         else rj = jt - d + c + (idx - 2 * wd - hd), rk = kb + kTK - 1 + d;
     };
-    int rg[RP], ro0[RP];  // ring (0: none) and A-frame offset
+    int rg[RP], ro0[RP], rb0[RP];  // ring (0: none), A-frame and B-slot offsets
     unsigned ra_off[RP];  // seam-partner load offsets (kOOB when masked)
     bool rcd[RP];         // stencil-valued node (else 0: Dirichlet face)
     int ry[RP], rx[RP];
@@ -423,6 +411,7 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(1,
         rg[s] = g;
         ry[s] = rj - jt + D, rx[s] = rk - kb + D;
         ro0[s] = Gm::at(0, ry[s], rx[s]);
+        rb0[s] = Gm::bat(ry[s], rx[s]);
         rcd[s] = g != 0 && incd(rj, rk);
         ra_off[s] = boff(rj, rk, g != 0 && inb(rj, rk));
     }
@@ -435,21 +424,40 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(1,
     static_assert(Gm::RPW == 3, "dma_fill3: three slot rows per wave");
     const unsigned sjb = unsigned(sj) * ES;
     const unsigned src0 = unsigned((jt - D + w * Gm::RPW) * sj + kb - D + p.poff) * ES;
-    const unsigned lds0 = unsigned(w * Gm::RPW * W0 * ES);
+    const unsigned lds0 = unsigned(w * Gm::RPW * W0 * ES), bds0 = unsigned(w * Gm::RPW * Gm::W(1) * ES);
     auto fillA = [&](auto qc, int plane, bool live) {
         dma_fill3<ES, W0 * ES, Gm::rowb>(prs(p.A, plane, live ? pbytes : 0u), src0, sjb, lds_addr(Ap(qc)), lds0);
     };
-    auto fillB = [&](auto qc, int plane, bool live) {
-        dma_fill3<ES, W0 * ES, Gm::rowb>(prs(p.B, plane, live ? pbytes : 0u), src0, sjb, lds_addr(Bp(qc)), lds0);
+    auto fillB = [&](int q, int plane, bool live) {
+        dma_fill3<ES, Gm::W(1) * ES, Gm::browb>(prs(p.B, plane, live ? pbytes : 0u), src0 + ES, sjb,
+                                                __builtin_amdgcn_readfirstlane(lds_addr(Bp(q))), bds0);
     };
-    // VM operations a steady plane issues after its DMA pieces: the stores of its last two layers
-    constexpr int NST = 2 * R;
-    // prologue: A(i0-1), A(i0), A(i0+1) into slots 0..2 (A(x) in slot (x - i0 + 1) & 3), B(i0)
-    // into slot 0 (B(x) in slot (x - i0) & 1)
-    fillA(Ic<0>{}, i0 - 1, true);
-    fillA(Ic<1>{}, i0, true);
-    fillA(Ic<2>{}, i0 + 1, true);
-    if constexpr (!FIRST) fillB(Ic<0>{}, i0, true);
+    // Two planes of lookahead for A and B: A(x) in A slot (x - i0) & 3 — A(i), A(i+1) read at
+    // iteration i, A(i+2) in flight, A(i+3) issued into the slot of A(i-1), whose own-node and
+    // ring values ride in registers from the last iteration (aw / raw: its x- neighbour for layer
+    // 0, U_{-1} for layer 1); B(x) in B slot (x - i0) mod 3 — B(i) read, B(i+1) in flight, B(i+2)
+    // issued into the slot of B(i-1). Each iteration issues its A pieces, then its B pieces, then
+    // its stores; a steady iteration waits for what iteration i-2 issued, i.e. for all but the
+    // operations of iteration i-1 and the stores of i-2: NDMA + 2 NST.
+    constexpr int NST = 2 * R;                                  // stores of the last two layers
+    constexpr int NDMA = ES == 8 ? 2 * Gm::RPW : 4 * Gm::RPW;  // pieces per iteration (A + B)
+    // prologue: A(i0-1) .. A(i0+2) into slots 3, 0, 1, 2; B(i0), B(i0+1) into slots 0, 1; then
+    // A(i0-1)'s register copies
+    fillA(Ic<3>{}, i0 - 1, true);
+    fillA(Ic<0>{}, i0, true);
+    fillA(Ic<1>{}, i0 + 1, true);
+    fillA(Ic<2>{}, i0 + 2, true);
+    if constexpr (!FIRST) {
+        fillB(0, i0, true);
+        fillB(1, i0 + 1, true);
+    }
+    vm_wait<0>();
+    __syncthreads();
+    T aw[2][R], raw[2][RP];  // A of the own rows / ring slots in a plane-parity slot (iteration i: A(i) in i - i0 & 1)
+#pragma unroll
+    for (int r = 0; r < R; ++r) aw[0][r] = T(0), aw[1][r] = ldsr(Ap(Ic<3>{}), Gm::at(0, D + w * R + r, D + lane));
+#pragma unroll
+    for (int s = 0; s < RP; ++s) raw[0][s] = T(0), raw[1][s] = ldsr(Ap(Ic<3>{}), ro0[s]);
 
     // slots (iteration i = i0 + q, phase P = q & 3): U_l(x) (x + l - i0) & 3 -> U_l of this
     // iteration in P, of the last in P+3, of the one before in P+2
@@ -560,19 +568,18 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(1,
         constexpr bool FAST = !ALIAS;
         constexpr int S0 = P & 3, S1 = (P + 1) & 3, S2 = (P + 2) & 3, S3 = (P + 3) & 3;
         constexpr int H0 = P & 1, H1 = (P + 1) & 1;
-        // A(i-1) .. A(i+2) in A slots S0 .. S3, B(i) / B(i+1) in B slots H0 / H1
+        // A(i) .. A(i+3) in A slots S0 .. S3; B(i) in B slot bq, B(i+2) into bq + 2 (mod 3)
+        const int bq = (i - i0) % 3;
 
-        // ---- A(i+1), B(i) landed (issued one iteration ago: everything but the stores that
-        // followed them; the checked body waits for all) -> barrier -> DMA B(i+1), A(i+2) into
-        // the slots of B(i-1), A(i-2), whose last readers passed the barrier
-        if constexpr (FAST) vm_wait<NST>();
+        // ---- what iteration i-2 issued has landed (A(i+1), B(i); the checked body waits for
+        // everything) -> barrier -> DMA A(i+3), B(i+2) into the slots of A(i-1), B(i-1), whose
+        // last readers passed the barrier
+        if constexpr (FAST) vm_wait<NDMA + 2 * NST>();
         else vm_wait<0>();
         __syncthreads();
-        auto fills = [&]() {
-            if constexpr (!FIRST) fillB(Ic<H1>{}, i + 1, FAST || i + 1 <= ie + D - 1);
-            fillA(Ic<S3>{}, i + 2, FAST || i + 2 <= ie + D);
-        };
-        if constexpr (W3D_TBN_DMAPOS == 0) fills();
+        // (issued right here: later in the plane measured 7-16 % slower)
+        fillA(Ic<S3>{}, i + 3, FAST || i + 3 <= ie + D);
+        if constexpr (!FIRST) fillB(bq == 0 ? 2 : bq - 1, i + 2, FAST || i + 2 <= ie + D - 1);
 
         T ev[R];  // U_{D-1}(i - D + 1): stored and its errors taken below
 #pragma unroll
@@ -580,16 +587,15 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(1,
         // staged layer l at frame offset o: A(i) for layer 0, U_{l-1} of the last iteration else
         auto St = [&](auto lc, int o) -> T {
             constexpr int l = decltype(lc)::value;
-            if constexpr (l == 0) return ldsr(Ap(Ic<S1>{}), o);
+            if constexpr (l == 0) return ldsr(Ap(Ic<S0>{}), o);
             else return ldsr(Up(lc, Ic<H1>{}), o);
         };
-        // ---- a layer's LDS reads, own nodes and ring together (one LDS round trip per layer):
-        // issued ahead of the previous layer's arithmetic and writes (they read the frames of
-        // the last iteration, other objects than this iteration's writes) and pinned — waited
-        // for — before the layer's own arithmetic (W3D_TBN_PIPE; 0: after the previous layer)
+        // ---- a layer's LDS reads, own nodes and ring together (one LDS round trip per layer);
+        // issuing the next layer's ahead of this layer's arithmetic measured no faster, even
+        // with the registers for it (profiles/deep_sweeps_r5.txt)
         struct Gath {
-            T gy[R][2], gz[R][2], gc[R], gxm[R], gxp[R], gpw[R];
-            T grn[RP][4], grc[RP], grxm[RP], grxp[RP], grpw[RP];
+            T gy[R][2], gz[R][2], gc[R], gxp[R], gpw[R];
+            T grn[RP][4], grc[RP], grxp[RP], grpw[RP];
         };
         Gath gt[2];
         auto gather = [&](auto lc) {
@@ -604,10 +610,8 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(1,
                 if (r == R - 1) g.gy[r][1] = St(lc, o + Wl);
                 g.gz[r][0] = St(lc, o - 1), g.gz[r][1] = St(lc, o + 1);
                 if constexpr (l == 0) {
-                    g.gc[r] = ldsr(Ap(Ic<S1>{}), oA), g.gxm[r] = ldsr(Ap(Ic<S0>{}), oA), g.gxp[r] = ldsr(Ap(Ic<S2>{}), oA);
-                    if constexpr (!FIRST) g.gpw[r] = ldsr(Bp(Ic<H0>{}), oA);
-                } else if constexpr (l == 1 && !DELTA) {
-                    g.gpw[r] = ldsr(Ap(Ic<S0>{}), oA);  // U_{-1} = A(i-1)
+                    g.gc[r] = ldsr(Ap(Ic<S0>{}), oA), g.gxp[r] = ldsr(Ap(Ic<S1>{}), oA);
+                    if constexpr (!FIRST) g.gpw[r] = ldsr(Bp(bq), Gm::bat(y, xx));
                 }
             }
             if constexpr (l <= D - 2)
@@ -618,58 +622,33 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(1,
                         g.grn[s][0] = St(lc, ro - Wl), g.grn[s][1] = St(lc, ro + Wl);
                         g.grn[s][2] = St(lc, ro - 1), g.grn[s][3] = St(lc, ro + 1);
                         if constexpr (l == 0) {
-                            g.grc[s] = ldsr(Ap(Ic<S1>{}), ro0[s]), g.grxm[s] = ldsr(Ap(Ic<S0>{}), ro0[s]);
-                            g.grxp[s] = ldsr(Ap(Ic<S2>{}), ro0[s]);
-                            if constexpr (!FIRST) g.grpw[s] = ldsr(Bp(Ic<H0>{}), ro0[s]);
-                        } else if constexpr (l == 1 && !DELTA) {
-                            g.grpw[s] = ldsr(Ap(Ic<S0>{}), ro0[s]);
+                            g.grc[s] = ldsr(Ap(Ic<S0>{}), ro0[s]), g.grxp[s] = ldsr(Ap(Ic<S1>{}), ro0[s]);
+                            if constexpr (!FIRST) g.grpw[s] = ldsr(Bp(bq), rb0[s]);
                         }
                     }
                 });
         };
-        // the ring values are consumed inside the ring branch: unpinned, LLVM sinks their loads
-        // into it, behind the own nodes' LDS writes (a second LDS round trip per layer)
-        auto pin_ring = [&](auto lc) {
-            constexpr int l = decltype(lc)::value;
-            Gath& g = gt[l & 1];
-            if constexpr (W3D_TBN_PIN && !W3D_TBN_VOL && l <= D - 2)
-                sfor<RP>([&](auto sc) {
-                    constexpr int s = decltype(sc)::value;
-                    if constexpr (Gm::ring_of(s * NT) <= D - 1 - l) {
-                        sfor<4>([&](auto nc) { pin(g.grn[s][decltype(nc)::value]); });
-                        if constexpr (l == 0) {
-                            pin(g.grc[s]), pin(g.grxm[s]), pin(g.grxp[s]);
-                            if constexpr (!FIRST) pin(g.grpw[s]);
-                        } else if constexpr (l == 1 && !DELTA) {
-                            pin(g.grpw[s]);
-                        }
-                    }
-                });
-        };
-        if constexpr (W3D_TBN_PIPE) gather(Ic<0>{}), pin_ring(Ic<0>{});  // layer 0: nothing to overlap
         sfor<D>([&](auto lc) {
             constexpr int l = decltype(lc)::value;
             const int x = i - l;
-            if constexpr (W3D_TBN_PIPE) {
-                if constexpr (l + 1 < D) gather(Ic<l + 1>{});
-                if constexpr (l > 0) pin_ring(lc);
-            } else {
-                gather(lc), pin_ring(lc);
-                // the DMA pieces after this layer's LDS reads (W3D_TBN_DMAPOS = l + 1)
-                if constexpr (W3D_TBN_DMAPOS == l + 1) fills();
-            }
+            gather(lc);
             Gath& g = gt[l & 1];
             auto& gy = g.gy;
             auto& gz = g.gz;
             auto& gc = g.gc;
-            auto& gxm = g.gxm;
             auto& gxp = g.gxp;
             auto& gpw = g.gpw;
             auto& grn = g.grn;
             auto& grc = g.grc;
-            auto& grxm = g.grxm;
             auto& grxp = g.grxp;
             auto& grpw = g.grpw;
+            // A(i) of the own rows and ring slot: next iteration's A(i-1) (register window)
+            if constexpr (l == 0) {
+#pragma unroll
+                for (int r = 0; r < R; ++r) aw[H0][r] = gc[r];
+#pragma unroll
+                for (int s = 0; s < RP; ++s) raw[H0][s] = grc[s];
+            }
             if (!(FAST || (x >= ib - (D - 1 - l) && x <= ie + (D - 1 - l)))) return;
             // ---- own nodes ----
             T v[R], dl[R];  // dl: the increment form's d of the last layer (stored to O[0])
@@ -678,11 +657,11 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(1,
                 const int y = D + w * R + r, xx = D + lane;
                 T ctr, xm, xp, pw = T(0);
                 if constexpr (l == 0) {
-                    ctr = gc[r], xm = gxm[r], xp = gxp[r];
+                    ctr = gc[r], xm = aw[H1][r], xp = gxp[r];
                     if constexpr (!FIRST) pw = gpw[r];
                 } else {
                     ctr = u[l - 1][S3][r], xp = u[l - 1][S0][r], xm = u[l - 1][S2][r];
-                    if constexpr (l == 1 && !DELTA) pw = gpw[r];
+                    if constexpr (l == 1 && !DELTA) pw = aw[H1][r];  // U_{-1} = A(i-1)
                     else if constexpr (l >= 2) pw = u[l - 2][S2][r];
                 }
                 if constexpr (ALIAS && l <= D - 2) {
@@ -717,11 +696,11 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(1,
                         if (rg[s] >= 1 && rg[s] <= D - 1 - l) {
                             T ctr, xm, xp, pw = T(0);
                             if constexpr (l == 0) {
-                                ctr = grc[s], xm = grxm[s], xp = grxp[s];
+                                ctr = grc[s], xm = raw[H1][s], xp = grxp[s];
                                 if constexpr (!FIRST) pw = grpw[s];
                             } else {
                                 ctr = ru[s][l - 1][S3], xp = ru[s][l - 1][S0], xm = ru[s][l - 1][S2];
-                                if constexpr (l == 1 && !DELTA) pw = grpw[s];
+                                if constexpr (l == 1 && !DELTA) pw = raw[H1][s];
                                 else if constexpr (l >= 2) pw = ru[s][l - 2][S2];
                             }
                             if constexpr (ALIAS) {
@@ -774,7 +753,7 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(1,
 
         // ---- errors of plane e = i - (D-1), every layer ----------------------------------------
         const int e = i - (D - 1);
-        if (FAST || (e >= ib && e <= ie)) {
+        if ((FAST || (e >= ib && e <= ie)) && !W3D_TBN_ABL_ERR) {
             constexpr int HE = (P + 4 - (D - 1)) & 1;  // table row slot of plane e
             const bool eplane = FAST || (e >= p.ei0 && e <= p.ei1);
             T fb[R];
@@ -796,9 +775,12 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(1,
                     else val[r] = u[l][SE][r];
                 }
                 if constexpr (FM) {
+                    // chk (the non-finite detector) on the last layer only: a NaN / Inf in layer
+                    // l reaches U_{D-1} at the same node within the sweep (through the centre
+                    // term, masked nodes included), so the sweep's last layer carries the flag
 #pragma unroll
                     for (int r = 0; r < R; ++r) {
-                        chk[l] = fma_t(val[r], om[r], chk[l]);
+                        if constexpr (l == D - 1) chk[l] = fma_t(val[r], om[r], chk[l]);
                         const T dv = (val[r] - fb[r] * p.ct[l]) * m[r];
                         ma[l] = max_abs(ma[l], dv);
                         mr[l].add(dv, wq[r]);
@@ -808,13 +790,13 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(1,
 #pragma unroll
                         for (int r = 0; r < R; ++r) {
                             if (!ovalid[r]) continue;
-                            chk[l] += val[r];
+                            if constexpr (l == D - 1) chk[l] += val[r];
                             accumulate_error_dev(val[r], fb[r] * p.ct[l], ma[l], mr[l]);
                         }
                     } else {
 #pragma unroll
                         for (int r = 0; r < R; ++r)
-                            if (ovalid[r]) chk[l] += val[r];
+                            if (l == D - 1 && ovalid[r]) chk[l] += val[r];
                     }
                 }
             });
@@ -852,8 +834,8 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(1,
     for (int pass = 0; pass < 2; ++pass) {
         checked(i, pass == 0 ? min(fstart, iend + 1) : iend + 1);
         if (pass == 0 && i == fstart) {  // (a work item shorter than the window start ran through)
-            // the steady body's counted wait assumes its predecessor issued NST operations
-            // after its DMA pieces; the checked body's may differ: drain them here
+            // the steady body's counted wait assumes its two predecessors issued exactly their
+            // pieces and NST stores; the checked body's stores may differ: drain them here
             vm_wait<0>();
             for (; i < fend; i += 4) {
                 plane(Ph<0>{}, std::false_type{}, i);
