@@ -255,7 +255,10 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(1,
     // cannot alias, so the compiler may hoist a layer's LDS reads above the previous layer's
     // writes; fp32 one array (measured faster there, profiles/deep_sweeps_r4.txt batches 21/30)
     constexpr bool ONE = sizeof(T) == 4;
-    __shared__ T lds[ONE ? Gm::total : 1];
+#ifndef W3D_TBN_LDSPAD  // diagnostics: extra LDS elements (fewer workgroups per CU)
+#define W3D_TBN_LDSPAD 0
+#endif
+    __shared__ T lds[ONE ? Gm::total + W3D_TBN_LDSPAD : 1];
     constexpr int ZA = ONE ? 1 : Gm::scells, ZB = ONE ? 1 : 3 * Gm::bcells, Z1 = ONE ? 1 : Gm::cells(1);
     constexpr int Z2 = ONE || D <= 2 ? 1 : Gm::cells(2), Z3 = ONE || D <= 3 ? 1 : Gm::cells(3);
     __shared__ T tA0[ZA], tA1[ZA], tA2[ZA], tA3[ZA], tB[ZB];
@@ -440,7 +443,8 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(1,
     // its stores; a steady iteration waits for what iteration i-2 issued, i.e. for all but the
     // operations of iteration i-1 and the stores of i-2: NDMA + 2 NST.
     constexpr int NST = 2 * R;                                  // stores of the last two layers
-    constexpr int NDMA = ES == 8 ? 2 * Gm::RPW : 4 * Gm::RPW;  // pieces per iteration (A + B)
+    // pieces per iteration: A, and B unless this is the first sweep (which reads no B)
+    constexpr int NDMA = (ES == 8 ? 1 : 2) * Gm::RPW * (FIRST ? 1 : 2);
     // prologue: A(i0-1) .. A(i0+2) into slots 3, 0, 1, 2; B(i0), B(i0+1) into slots 0, 1; then
     // A(i0-1)'s register copies
     fillA(Ic<3>{}, i0 - 1, true);

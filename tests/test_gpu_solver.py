@@ -628,3 +628,22 @@ def test_tb4_delta_fp64_is_refused(C):
     with pytest.raises(Exception, match="increment form"):
         _solve(p, kernel="tb4")
     assert _solve(p).kernel != "tb4"
+
+
+@pytest.mark.parametrize("dtype", ["fp64", "fp32"])
+@pytest.mark.parametrize("math_", ["exact", "fma"])
+def test_tb4_repeat_solves_identical(C, dtype, math_):
+    """The LDS-DMA four-layer sweeps give the same per-layer errors on every solve of a session
+    (a counted-wait mistake — e.g. the first sweep, which stages no B — shows up as a solve that
+    differs), and fp64 the OpenMP oracle's bit for bit. N=200 tiles every tile row and column
+    with partial last tiles; 8 sweeps include the first."""
+    import wave3d
+
+    p = wave3d.WaveProblem(200, timesteps=33, ic="shifted", dtype=dtype, math=math_)
+    s = wave3d.WaveSolver(p, "hip", kernel="tb4")
+    runs = [s.run() for _ in range(5)]
+    for r in runs[1:]:
+        assert r.max_abs == runs[0].max_abs and r.max_rel == runs[0].max_rel
+    if dtype == "fp64":
+        c = _solve(p, backend="cpu", threads=8)
+        assert runs[0].max_abs == c.max_abs
