@@ -31,40 +31,10 @@
 
 #include "device_common.hpp"
 
-// timing ablations of the sweep (tools/ab_tb3_abl.sh builds; never the shipped library):
-// 1 = no error accumulation, 3 = no ring C/D, 4 = every load and store on one fixed plane (no
-// HBM traffic: the compute / LDS / barrier bound), 5 = stores only on one plane, 6 = loads only
-#ifndef W3D_TB3_ABL
-#define W3D_TB3_ABL 0
-#endif
-// LDS row pitch padding (doubles/floats added to the even tile widths): 1 makes the pitches odd,
-// so a ring column (lanes at one k, consecutive rows) hits 32 distinct ds_read_b64 bank pairs
-#ifndef W3D_TB3_SPLIT  // A/B: 0 = one loop choosing the plane body per plane
-#define W3D_TB3_SPLIT 1
-#endif
-#ifndef W3D_TB3_MASKMUL  // A/B: fp64 face masks and the fma checksum as products (cmask)
-#define W3D_TB3_MASKMUL 1
-#endif
-#ifndef W3D_TB3_ONE_LDS  // A/B: 1 = the double-buffered tiles as [2] arrays (one object each)
-#define W3D_TB3_ONE_LDS 0
-#endif
-// A/B: wave priority raised (s_setprio) while a plane's prefetch loads and A staging issue
-#ifndef W3D_TB3_PRIO
-#define W3D_TB3_PRIO 0
-#endif
-// A/B: 1 = the j neighbours of a wave's own rows that are its other own rows come from registers
-// (the centre values it already holds) instead of LDS, as k_tbn does
-#ifndef W3D_TB3_JREG
-#define W3D_TB3_JREG 1
-#endif
-#ifndef W3D_TB3_PAD
-#define W3D_TB3_PAD 0
-#endif
-// B slots: 2 = B(i+1) prefetched at iteration i, 4 = B(i+2) (two planes of load latency)
-#ifndef W3D_TB3_NB
-#define W3D_TB3_NB 2
-#endif
-
+// The measured winners of round 3-4's A/B switches are built in (profiles/deep_sweeps_r4.txt,
+// tb3_mem_ablation_r4.txt): the plane loop split into checked / steady bodies, fp64 face masks
+// as products, one __shared__ object per staged tile and buffer, register j-neighbours, odd LDS
+// pitches only where they came for free, B one plane ahead, no wave-priority bumps.
 namespace wave3d {
 namespace {
 
@@ -125,32 +95,23 @@ template <class T, bool FIRST, int R, int NW, bool DELTA = false, bool FM = fals
           int WPE = (R == 1 || (DELTA && sizeof(T) == 4) ? 4 : 1)>
 __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WPE, 8))) k_tb3(const Tb3Params<T> p) {
     constexpr int TJ = NW * R;
-    constexpr int AH = TJ + 6, AW = kTK + 6 + W3D_TB3_PAD;  // A tile origin (jt-3, kb-3)
-    constexpr int CH = TJ + 4, CW = kTK + 4 + W3D_TB3_PAD;  // C tile origin (jt-2, kb-2)
-    constexpr int DH = TJ + 2, DW = kTK + 2 + W3D_TB3_PAD;  // D tile origin (jt-1, kb-1)
+    constexpr int AH = TJ + 6, AW = kTK + 6;  // A tile origin (jt-3, kb-3)
+    constexpr int CH = TJ + 4, CW = kTK + 4;  // C tile origin (jt-2, kb-2)
+    constexpr int DH = TJ + 2, DW = kTK + 2;  // D tile origin (jt-1, kb-1)
     constexpr int N1 = 2 * kTK + 2 * (TJ + 2);        // 1-ring positions
     constexpr int N2 = 2 * (kTK + 2) + 2 * (TJ + 4);  // 2-ring positions
     constexpr int N3 = 2 * (kTK + 4) + 2 * (TJ + 4);  // 3-ring positions (A only, no corners)
     constexpr int NT = NW * 64;
     constexpr int RP = (N1 + N2 + N3 + NT - 1) / NT;  // ring positions per thread
     constexpr unsigned ES = sizeof(T);
-    // one __shared__ object per staged tile and buffer (W3D_TB3_ONE_LDS = 0): distinct objects
-    // cannot alias, so the compiler may move a tile's LDS reads past another tile's writes
-#if W3D_TB3_ONE_LDS
-    __shared__ T ldsA[2][AH][AW];
-    __shared__ T ldsC[2][CH][CW];
-    __shared__ T ldsD[2][DH][DW];
-    auto LA = [&](int h) -> T(*)[AW] { return ldsA[h]; };
-    auto LC = [&](int h) -> T(*)[CW] { return ldsC[h]; };
-    auto LD = [&](int h) -> T(*)[DW] { return ldsD[h]; };
-#else
+    // one __shared__ object per staged tile and buffer: distinct objects cannot alias, so the
+    // compiler may move a tile's LDS reads past another tile's writes
     __shared__ T ldsA0[AH][AW], ldsA1[AH][AW];
     __shared__ T ldsC0[CH][CW], ldsC1[CH][CW];
     __shared__ T ldsD0[DH][DW], ldsD1[DH][DW];
     auto LA = [&](int h) -> T(*)[AW] { return h ? ldsA1 : ldsA0; };
     auto LC = [&](int h) -> T(*)[CW] { return h ? ldsC1 : ldsC0; };
     auto LD = [&](int h) -> T(*)[DW] { return h ? ldsD1 : ldsD0; };
-#endif
 
     const int bid = blockIdx.x;
     const int b = find_box(p, bid);
@@ -195,11 +156,9 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WP
     };
     // timing ablations 4-6: loads (A, B) / stores (D, E) pinned to one plane (wrong results)
     auto prl = [&](const char* base, int i, unsigned nb) {
-        if (W3D_TB3_ABL == 4 || W3D_TB3_ABL == 6) i = ib;
         return prs(base, i, nb);
     };
     auto pst = [&](char* base, int i, unsigned nb) {
-        if (W3D_TB3_ABL == 4 || W3D_TB3_ABL == 5) i = ib;
         return prs(base, i, nb);
     };
     auto lrs = [&](const T* plane) { return plane_rsrc(plane - p.poff, pbytes); };
@@ -224,9 +183,9 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WP
     T om[R];  // --math fma: 1 on valid own nodes, 0 on masked lanes (branch-free errors)
 #pragma unroll
     for (int r = 0; r < R; ++r) om[r] = ovalid[r] ? T(1) : T(0);
-    // Dirichlet-face masks of computed values: a select, or (W3D_TB3_MASKMUL, fp64) a product
+    // Dirichlet-face masks of computed values: a select (fp32) or a product (fp64)
     // with a 0/1 register — one op instead of two v_cndmask, and no lane masks held in SGPRs
-    constexpr bool MM = W3D_TB3_MASKMUL && sizeof(T) == 8;
+    constexpr bool MM = sizeof(T) == 8;
     T ocm[R];
 #pragma unroll
     for (int r = 0; r < R; ++r) ocm[r] = ocd[r] ? T(1) : T(0);
@@ -296,7 +255,7 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WP
     //   C(x), ring C(x): (x - ib + 2) & 3  -> C(i) = P, C(i-1) = P+3, C(i-2) = P+2
     //   D(x): (x - ib + 3) & 3             -> D(i-1) = P, D(i-2) = P+3, D(i-3) = P+2
     //   B(x), ring B(x), LDS buffers: (x - ib + 2) & 1
-    constexpr int NB = W3D_TB3_NB, BD = NB / 2;  // B slots, B prefetch distance (planes)
+    constexpr int NB = 2, BD = 1;  // B slots, B prefetch distance (planes)
     T a[4][R], c[4][R], d[4][R], bb[NB][R];
     T ra[RP][4], rb[RP][NB], rc[RP][4];
     // increment form: d^m of own planes i (H0) / i-1 (H1) and of the ring, d^{m+1} of own
@@ -370,10 +329,10 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WP
     // own row r's j neighbours: rows r-1 / r+1 of the same wave are centre values in registers
     // (v[], as staged to LDS at (y -/+ 1, x)); the wave's edge rows read the tile
     auto jm = [&](const T(&v)[R], int r, const auto& tile, int y, int x) {
-        return (W3D_TB3_JREG && r > 0) ? v[r > 0 ? r - 1 : 0] : tile[y - 1][x];
+        return (r > 0) ? v[r > 0 ? r - 1 : 0] : tile[y - 1][x];
     };
     auto jp = [&](const T(&v)[R], int r, const auto& tile, int y, int x) {
-        return (W3D_TB3_JREG && r < R - 1) ? v[r < R - 1 ? r + 1 : 0] : tile[y + 1][x];
+        return (r < R - 1) ? v[r < R - 1 ? r + 1 : 0] : tile[y + 1][x];
     };
     auto cval = [&](T ctr, T bv, const auto& l) {
         if constexpr (FM) return FIRST ? ctr + lap_value(l) : l.leap(bv, kc1);
@@ -425,9 +384,6 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WP
     // running maxima; the relative weight wq = 1/|sx sy| * 1/|sz| is shared by the three layers
     auto errors_fm = [&](const T(&v)[R], const T(&fb)[R], const T(&m)[R], const T(&wq)[R], const T ct, T& ma,
                          RelMax<T>& mr, T& chk) {
-#if W3D_TB3_ABL == 1
-        return;
-#endif
 #pragma unroll
         for (int r = 0; r < R; ++r) {
             if constexpr (MM) chk = fma_t(v[r], om[r], chk);
@@ -470,7 +426,6 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WP
         constexpr int BC = P & (NB - 1), BP = (P + BD) & (NB - 1);  // B(i), B(i+BD) slots
 
         // ---- prefetch A(i+2), B(i+BD) (own and ring; 0-record descriptors when done) -------
-        if constexpr (W3D_TB3_PRIO > 0) __builtin_amdgcn_s_setprio(W3D_TB3_PRIO);
         {
             const bool more = FAST || i <= ie + 1, moreB = FAST || i + BD <= ie + 2;
             const unsigned nb = more ? pbytes : 0u;
@@ -494,7 +449,6 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WP
 #pragma unroll
         for (int s = 0; s < RP; ++s)
             if (rg[s]) LA(H0)[ry[s]][rx[s]] = ra[s][S1];
-        if constexpr (W3D_TB3_PRIO > 0) __builtin_amdgcn_s_setprio(0);
         __syncthreads();
 
         // ---- seam partners (uniform branch, rare) -------------------------------------------
@@ -554,7 +508,7 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WP
         }
 #pragma unroll
         for (int s = 0; s < RP; ++s) {
-            if (W3D_TB3_ABL != 3 && (rg[s] == 1 || rg[s] == 2)) {
+            if (rg[s] == 1 || rg[s] == 2) {
                 const auto lap = lapA(H0, ry[s], rx[s], ra[s][S1], rxp[s], rxn[s]);
                 T cv;
                 if constexpr (DELTA) {
@@ -602,7 +556,7 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WP
             }
 #pragma unroll
             for (int s = 0; s < RP; ++s) {
-                if (W3D_TB3_ABL != 3 && rg[s] == 1) {
+                if (rg[s] == 1) {
                     const int y = ry[s] - 1, x = rx[s] - 1;
                     const auto l = lap(1, rc[s][S3], rcp[s], rcn[s], LC(H1)[y - 1][x], LC(H1)[y + 1][x],
                                     LC(H1)[y][x - 1], LC(H1)[y][x + 1]);
@@ -679,7 +633,6 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WP
         load_row(H1, i - 1);
     };
 
-#if W3D_TB3_SPLIT
     // i = ib-2 .. ie+2 (>= 5 planes) in three loops, each unrolled by 4 from phase 0 so every
     // slot index is a constant: the checked body (ALIAS: seam / wrap / work-item ends) up to the
     // first phase-0 plane of the steady window [flo, fhi], the steady body over whole groups of 4
@@ -713,24 +666,6 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WP
                 plane(Ph<3>{}, std::false_type{}, i + 3);
             }
     }
-#else
-    auto step = [&](auto phase, const int i) {
-        if (i < flo || i > fhi) plane(phase, std::true_type{}, i);  // seam / wrap / ends
-        else plane(phase, std::false_type{}, i);
-    };
-
-    // i = ib-2 .. ie+2 (>= 5 planes), unrolled by 4 so every slot index is a constant
-    for (int i = ib - 2;;) {
-        step(Ph<0>{}, i);
-        if (++i > ie + 2) break;
-        step(Ph<1>{}, i);
-        if (++i > ie + 2) break;
-        step(Ph<2>{}, i);
-        if (++i > ie + 2) break;
-        step(Ph<3>{}, i);
-        if (++i > ie + 2) break;
-    }
-#endif
     auto rel = [&](const Rel& m, int L) {
         if constexpr (FM) return m.value(p.ict[L]);
         else return m.value();
