@@ -47,9 +47,10 @@ std::string usage() {
            "  --rccl-mirror          with --ranks P: also send every halo message (and the error\n"
            "                         allreduce) through a 1-rank RCCL communicator, compare bitwise\n"
            "  --no-halo-check        skip the init-time halo self-test (patterns through the real plan)\n"
-           "  --model-link G[,L]     with --ranks P: every loopback exchange also waits the time its\n"
-           "                         busiest peer link needs at G GB/s (+ L us latency), on one CU\n"
-           "                         (an xGMI link model for overlap experiments on one GPU)\n"
+           "  --model-link G[,L]     every halo exchange also waits the time its busiest peer link\n"
+           "                         needs at G GB/s (+ L us latency), on one CU (an xGMI link model\n"
+           "                         for overlap experiments on one GPU: --ranks P, or processes\n"
+           "                         sharing it through the staged transport)\n"
            "  --device d  --threads t  --no-print-layers  --quiet\n";
 }
 

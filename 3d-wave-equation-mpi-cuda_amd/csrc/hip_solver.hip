@@ -1007,6 +1007,7 @@ private:
                 rcv.push_back({m.peer, m.tag, tb_ptr(R, m, mD), size_t(m.nplanes) * R.gv.si * sizeof(T)});
             for (auto& m : R.tb_psends) snd.push_back({m.peer, kPeerTag, m.buf, m.count * sizeof(T)});
             for (auto& m : R.tb_precvs) rcv.push_back({m.peer, kPeerTag, m.buf, m.count * sizeof(T)});
+            model_link_ext(snd, s);
             if (!snd.empty() || !rcv.empty()) ext_->exchange(snd, rcv, s);
         } else {
             std::map<std::pair<int, int>, size_t> link;
@@ -1063,6 +1064,7 @@ private:
                 rcv.push_back({m.peer, m.tag, tb_ptr(R, m, mD), size_t(m.nplanes) * R.gv.si * sizeof(T)});
             if (!snd.empty() || !rcv.empty()) {
                 mark(s, 6);
+                model_link_ext(snd, s);
                 ext_->exchange(snd, rcv, s);
                 mark(s, 7);
             }
@@ -1116,6 +1118,7 @@ private:
                 for (auto& m : R.tb_bsends[rd]) snd.push_back({m.peer, m.tag, m.buf, bytes(m)});
                 for (auto& m : R.tb_brecvs[rd]) rcv.push_back({m.peer, m.tag, m.buf, bytes(m)});
                 mark(s, 6);
+                model_link_ext(snd, s);
                 ext_->exchange(snd, rcv, s);
                 mark(s, 7);
             } else {
@@ -1383,6 +1386,7 @@ private:
                                size_t(R.plan.recvs[m].count) * sizeof(T)});
             if (!snd.empty() || !rcv.empty()) {
                 mark(s, 6);
+                model_link_ext(snd, s);
                 ext_->exchange(snd, rcv, s);
                 mark(s, 7);
             }
@@ -1427,6 +1431,16 @@ private:
     // bytes / bandwidth, plus one latency. One wave spins that long on the exchange stream (one
     // CU, as a remote transfer's kernels), so overlap experiments on one GPU see a halo that
     // costs wall time without costing the interior sweep its CUs.
+    // ... and for a rank of a distributed job (one process per GPU, or processes sharing one GPU
+    // through the staged transport): its own busiest outgoing link — every rank sends at once, so
+    // the exchange lasts about that long on every rank (bench.py --model-link rehearses the
+    // 8-GPU decompositions on one GPU with a link cost)
+    void model_link_ext(const std::vector<Message>& snd, hipStream_t s) {
+        if (cfg_.model_link_gbps <= 0 || snd.empty()) return;
+        std::map<std::pair<int, int>, size_t> link;
+        for (const auto& m : snd) link[{ranks_[0].topo.rank, m.peer}] += m.bytes;
+        model_link(link, s);
+    }
     void model_link(const std::map<std::pair<int, int>, size_t>& link_bytes, hipStream_t s) {
         if (cfg_.model_link_gbps <= 0) return;
         size_t most = 0;

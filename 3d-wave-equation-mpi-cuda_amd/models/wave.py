@@ -130,6 +130,8 @@ class WaveSolver:
     graph     "auto" | "on" | "off": replay the IC + time loop as one hipGraph
     transport a native transport (``parallel.rccl_transport()`` / ``TorchHostTransport``)
               making this process one rank of a distributed job
+    model_link "GBPS[,LAT_US]": every halo exchange also waits its busiest link's modelled time
+              (overlap rehearsals on one GPU, --model-link)
     """
 
     def __init__(self, problem: WaveProblem, backend: str = "hip", *, ranks: int = 0,
@@ -138,7 +140,7 @@ class WaveSolver:
                  out_dir: str | None = None, check_every: int = 0, fault: str | None = None,
                  checkpoint_every: int = 0, checkpoint_dir: str | None = None,
                  resume: str | None = None, profile: bool = False, device: int | None = None,
-                 graph: str = "auto"):
+                 graph: str = "auto", model_link: str | None = None):
         self.problem = problem
         self.backend = backend
         self.transport = transport
@@ -149,7 +151,8 @@ class WaveSolver:
                          out_dir=out_dir, check_every=check_every or None, fault=fault,
                          checkpoint_every=checkpoint_every or None,
                          checkpoint_dir=checkpoint_dir, resume=resume, profile=profile,
-                         device=device, graph=graph if backend == "hip" else None, quiet=True)
+                         device=device, graph=graph if backend == "hip" else None,
+                         model_link=model_link if backend == "hip" else None, quiet=True)
 
     def args(self, **extra) -> list[str]:
         o = dict(self.opts)

@@ -79,6 +79,9 @@ def main() -> int:
     ap.add_argument("--transport", default="rccl", choices=["rccl", "staged"],
                     help="halo transport for N>1 (staged = rehearsal on one shared GPU)")
     ap.add_argument("--shared-device", action="store_true", help="all ranks on device 0 (rehearsal)")
+    ap.add_argument("--model-link", default="",
+                    help="GBPS[,LAT_US]: each halo exchange also waits its busiest link's time at that "
+                         "bandwidth (the 8-GPU rehearsal on one GPU with an xGMI-like link cost)")
     ap.add_argument("--launch-timeout", type=float, default=1000.0,
                     help="self-launch (--gpus N without torchrun): kill every rank after this many s")
     a = ap.parse_args()
@@ -168,7 +171,8 @@ def main() -> int:
         print(f"bench: warning: C={prob.courant:.3f} > 1/sqrt(3) (unstable)", file=sys.stderr)
     solver = wave3d.WaveSolver(prob, a.backend, transport=transport, Np=n_gpus, kernel=a.kernel, dims=dims,
                                chunk=a.chunk, overlap="off" if a.no_overlap else a.overlap, profile=a.profile,
-                               device=(torch.cuda.current_device() if a.backend == "hip" else None))
+                               device=(torch.cuda.current_device() if a.backend == "hip" else None),
+                               model_link=a.model_link or None)
     args = solver.args()
     sess = C.Session(args, a.backend, transport)
 
@@ -236,6 +240,7 @@ def main() -> int:
             "overlap_order": res.get("overlap_order"),  # beside | shells_first (with overlap on)
             "overlap_trial_ms": list(res.get("overlap_trial_ms", (0, 0, 0))),  # best of two per arm
             "overlap_trials_ms": list(res.get("overlap_trials_ms", (0,) * 6)),
+            "model_link": a.model_link or None,  # rehearsal link model (GBPS[,LAT_US]), None = real links
             "transport": res["transport"],
             "hip_graph": bool(res.get("graph", False)),
             "fill_hbm": a.fill_hbm or None,

@@ -143,6 +143,26 @@ def test_bench_gpu_multirank_plan_staged(n, N, dims, golden):
 
 
 @pytest.mark.gpu
+def test_bench_gpu_model_link_rehearsal_records_the_arms():
+    """The 8-GPU bench shape rehearsed on one MI355X with an xGMI-like link cost (--model-link
+    50,5: every exchange also waits its busiest link's bytes at 50 GB/s + 5 us): 8 processes,
+    N=1024 on 2x2x2 at the golden L-inf; the JSON carries every --overlap auto trial, the arm kept
+    (overlap / overlap_order agree with the fastest best-of-two, ties to the earlier arm), the
+    link model and the RCCL CTA budget field (None without RCCL)."""
+    r = _bench(["--steps", "1", "--warmup", "7", "--transport", "staged", "--shared-device",
+                "--model-link", "50,5"], nproc=8, timeout=900)
+    c = r["config"]
+    assert c["dims"] == [2, 2, 2] and r["linf_ok"] is True and c["model_link"] == "50,5"
+    trials, (on, off, first) = c["overlap_trials_ms"], c["overlap_trial_ms"]
+    assert len(trials) == 6 and min(trials) > 0
+    assert on == min(trials[0], trials[3]) and off == min(trials[1], trials[4]) and first == min(trials[2], trials[5])
+    best = min(on, off, first)
+    kept = "beside" if on == best else ("none" if off == best else "shells_first")
+    assert c["overlap_order"] == kept and c["overlap"] == (kept != "none")
+    assert "rccl_max_ctas" in r and r["rccl_max_ctas"] is None
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("scheme,linf", [("leapfrog", "4.47035e-06"), ("auto", "1.3113e-06")])
 def test_bench_gpu_fp32_two_ranks_staged(scheme, linf):
     """fp32 runs the three-layer sweep (tb3, 3-deep halos) through the multi-process bench path:
