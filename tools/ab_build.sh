@@ -18,6 +18,7 @@ for v in "$@"; do
     for src in $srcs; do
       # the Makefile's per-object flags (NOSLP_OBJS), so a baseline arm builds the shipped code
       obj_flags=$(make -s -n build/hip/$src.o -W csrc/$src.hip 2>/dev/null | grep -o -- '-fno-slp-vectorize -mllvm -amdgpu-sched-strategy=[a-z-]*' | head -1)
+      [ -n "${AB_NO_OBJ_FLAGS:-}" ] && obj_flags=""
       $ROCM/bin/hipcc $FLAGS $obj_flags $extra -c csrc/$src.hip -o $out/$src.o
       vobjs="$vobjs $out/$src.o"
     done
