@@ -352,12 +352,17 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(1,
         oa[r] = boff(j, k, inb(j, k));
         os[r] = boff(j, k, ovalid[r]);
     }
-    const T otz = (k >= Bx.k0 && k <= Bx.k1) ? p.tz[k] : T(0);
     const T ortz = FM && k >= Bx.k0 && k <= Bx.k1 ? p.rtz[k] : T(0);
     const T* const txw = p.txy + (jt + w * R);
-    T om[R];  // --math fma: 1 on valid own nodes, 0 on masked lanes (branch-free errors)
+    // om: 1 on valid own nodes, 0 on masked lanes (the non-finite detector); otzr: sz, a quiet
+    // NaN on masked lanes — their analytic values and so their errors are NaN, which max_abs,
+    // RelMax and RelArg ignore (no product or branch per node: profiles/deep_sweeps_r5.txt)
+    T om[R], otzr[R];
 #pragma unroll
-    for (int r = 0; r < R; ++r) om[r] = ovalid[r] ? T(1) : T(0);
+    for (int r = 0; r < R; ++r) {
+        om[r] = ovalid[r] ? T(1) : T(0);
+        otzr[r] = nan_unless(ovalid[r], k >= Bx.k0 && k <= Bx.k1 ? p.tz[k] : T(0));
+    }
     // self-wrap ranges of O[0] / O[1] met by this work item (wave-uniform bits)
     int rare = 0;
 #pragma unroll
@@ -771,47 +776,35 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(1,
         if ((FAST || (e >= ib && e <= ie)) && !W3D_TBN_ABL_ERR) {
             constexpr int HE = (P + 4 - (D - 1)) & 1;  // table row slot of plane e
             const bool eplane = FAST || (e >= p.ei0 && e <= p.ei1);
-            T fb[R];
+            // (sx sy) sz: NaN on masked lanes (otzr) and outside the error planes
+            T fb[R], wq[R];
 #pragma unroll
-            for (int r = 0; r < R; ++r) fb[r] = tq[HE][r][0] * otz;  // (sx sy) sz
-            T m[R], wq[R];
-            if constexpr (FM) {
-                const T em = eplane ? T(1) : T(0);
-#pragma unroll
-                for (int r = 0; r < R; ++r) m[r] = FAST ? om[r] : om[r] * em, wq[r] = tq[HE][r][NQ - 1] * ortz;
+            for (int r = 0; r < R; ++r) {
+                fb[r] = tq[HE][r][0] * otzr[r];
+                if (!FAST && !eplane) fb[r] = nan_unless(false, fb[r]);
+                if constexpr (FM) wq[r] = tq[HE][r][NQ - 1] * ortz;
             }
             sfor<D>([&](auto lc) {
                 constexpr int l = decltype(lc)::value;
                 constexpr int SE = (P + 4 - (D - 1) + l) & 3;  // slot of U_l(e)
-                T val[R];
 #pragma unroll
                 for (int r = 0; r < R; ++r) {
-                    if constexpr (l == D - 1) val[r] = ev[r];
-                    else val[r] = u[l][SE][r];
-                }
-                if constexpr (FM) {
+                    T val;
+                    if constexpr (l == D - 1) val = ev[r];
+                    else val = u[l][SE][r];
                     // chk (the non-finite detector) on the last layer only: a NaN / Inf in layer
                     // l reaches U_{D-1} at the same node within the sweep (through the centre
                     // term, masked nodes included), so the sweep's last layer carries the flag
-#pragma unroll
-                    for (int r = 0; r < R; ++r) {
-                        if constexpr (l == D - 1) chk[l] = fma_t(val[r], om[r], chk[l]);
-                        const T dv = (val[r] - fb[r] * p.ct[l]) * m[r];
+                    if constexpr (l == D - 1) chk[l] = fma_t(val, om[r], chk[l]);
+                    if constexpr (FM) {
+                        const T dv = val - fb[r] * p.ct[l];
                         ma[l] = max_abs(ma[l], dv);
                         mr[l].add(dv, wq[r]);
-                    }
-                } else {
-                    if (eplane) {
-#pragma unroll
-                        for (int r = 0; r < R; ++r) {
-                            if (!ovalid[r]) continue;
-                            if constexpr (l == D - 1) chk[l] += val[r];
-                            accumulate_error_dev(val[r], fb[r] * p.ct[l], ma[l], mr[l]);
-                        }
                     } else {
-#pragma unroll
-                        for (int r = 0; r < R; ++r)
-                            if (l == D - 1 && ovalid[r]) chk[l] += val[r];
+                        const T f = fb[r] * p.ct[l];
+                        const T d = val - f;
+                        ma[l] = max_abs(ma[l], d);
+                        mr[l].add(d, f);
                     }
                 }
             });

@@ -11,6 +11,6 @@ for rep in $(seq "$rounds"); do
     echo -n "round=$rep $b $k deep=$d "
     WAVE3D_TBN_DEEP=$d timeout -k 10 ${TMO:-120} $W ${N:-512} 1 pi pi pi 1 ${K:-100} --math fma --kernel $k --repeat ${REP:-5} --warmup 1 \
         --json --quiet --format none ${EXTRA:-} \
-      | python3 -c "import sys,json; r=json.loads(sys.stdin.read().splitlines()[-1]); print(round(r['mpts_per_s_best']), '%.9g' % r['linf_abs'], r['kernel'])" || exit 1
+      | python3 -c "import sys,json; r=json.loads(sys.stdin.read().splitlines()[-1]); print(round(r['mpts_per_s_best']), '%.17g' % r['linf_abs'], '%.17g' % r['max_rel_final'], r['kernel'])" || exit 1
   done
 done
