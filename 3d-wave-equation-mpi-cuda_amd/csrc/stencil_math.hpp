@@ -180,6 +180,22 @@ W3D_HD T leap_fm(T c, T u2, T xm, T xp, T ym, T yp, T zm, T zp, T cx, T cy, T cz
         return leapfrog_fma(c, u2, coef_lap_fma(c, xm, xp, ym, yp, zm, zp, cx, cy, cz));
     }
 }
+// leap_fm with the Dirichlet mask m (1 computed node, 0 face / outside) in the last operation:
+// (2c - u2) + l*m, one rounding like the add for m = 1; on masked nodes c = u2 = 0 (the faces are
+// never stored), so the result is 0 without a product per node
+template <class T>
+W3D_HD T leap_fm_masked(T c, T u2, T xm, T xp, T ym, T yp, T zm, T zp, T cx, T cy, T cz, T kc, T m) {
+    if constexpr (W3D_FM_FUSED && std::is_same_v<T, double>) {
+        T t = cz * (zm + zp);
+        t = fma_t(cy, ym + yp, t);
+        t = fma_t(cx, xm + xp, t);
+        t = fma_t(kc, c, t);
+        return fma_t(t, m, fma_t(T(2), c, -u2));
+    } else {
+        (void)kc;
+        return fma_t(coef_lap_fma(c, xm, xp, ym, yp, zm, zp, cx, cy, cz), m, fma_t(T(2), c, -u2));
+    }
+}
 // A deferred --math fma stencil evaluation for the temporal-blocking kernels' lap() / leap()
 // lambdas: the leapfrog consumes the inputs whole (leap_fm), every other update (Taylor start,
 // increment form) takes coef*lap = value() — the same operations as before for those.
@@ -188,6 +204,9 @@ struct FmLap {
     T c, xm, xp, ym, yp, zm, zp, cx, cy, cz;
     W3D_HD T value() const { return coef_lap_fma(c, xm, xp, ym, yp, zm, zp, cx, cy, cz); }
     W3D_HD T leap(T u2, T kc) const { return leap_fm(c, u2, xm, xp, ym, yp, zm, zp, cx, cy, cz, kc); }
+    W3D_HD T leap_masked(T u2, T kc, T m) const {
+        return leap_fm_masked(c, u2, xm, xp, ym, yp, zm, zp, cx, cy, cz, kc, m);
+    }
 };
 template <class T>
 W3D_HD T lap_value(const FmLap<T>& l) {
