@@ -489,11 +489,11 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(1,
 
     // Dirichlet-face masks of the computed values: a product with a 0/1 register (one op; a
     // face value may become -0)
-    T ocm[R], rcm[RP], ocf[R], rcf[RP];  // masks and (exact) masked leapfrog coefficients
+    T ocm[R], rcm[RP];
 #pragma unroll
-    for (int r = 0; r < R; ++r) ocm[r] = ocd[r] ? T(1) : T(0), ocf[r] = ocd[r] ? p.coef[D - 1] : T(0);
+    for (int r = 0; r < R; ++r) ocm[r] = ocd[r] ? T(1) : T(0);
 #pragma unroll
-    for (int s = 0; s < RP; ++s) rcm[s] = rcd[s] ? T(1) : T(0), rcf[s] = rcd[s] ? p.coef[D - 1] : T(0);
+    for (int s = 0; s < RP; ++s) rcm[s] = rcd[s] ? T(1) : T(0);
     // increment form: d_l of the own rows / ring slots in a plane-parity slot (written at
     // iteration i for plane i - l, read by layer l+1 at iteration i+1: the same plane)
     constexpr int ND = DELTA ? D - 1 : 1, NRD = DELTA && D >= 3 ? D - 2 : 1;
@@ -541,19 +541,18 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(1,
     // memory, whose faces may hold the initial condition's analytic values (~1e-16, as in the
     // reference), so they multiply the result by m. From layer 2 on both come from masked
     // layers (exactly 0 there), and m rides in the last operation instead: fma(l, m, 2c - u2)
-    // (fma) or the masked coefficient cm = coef*m (exact: bitwise the same products for m = 1)
+    // (fma) or the masked coefficient coef*m (exact: bitwise the same products for m = 1)
     // — no product per node (profiles/deep_sweeps_r5.txt)
-    auto upd = [&](auto lc, T ctr, T pw, const auto& l_, T m, T cm) {
+    auto upd = [&](auto lc, T ctr, T pw, const auto& l_, T m) {
         constexpr int l = decltype(lc)::value;
         if constexpr (FM) {
-            (void)cm;
             if constexpr (FIRST && l == 0) return (ctr + lap_value(l_)) * m;
             else if constexpr (l <= 1) return l_.leap(pw, kc1) * m;
             else return l_.leap_masked(pw, kc1, m);
         } else {
             if constexpr (FIRST && l == 0) return taylor_first(ctr, l_, p.coef[0]) * m;
             else if constexpr (l <= 1) return leapfrog(ctr, pw, l_, p.coef[l]) * m;
-            else return leapfrog(ctr, pw, l_, cm);
+            else return leapfrog(ctr, pw, l_, p.coef[l] * m);  // loop-invariant product
         }
     };
 
@@ -710,7 +709,7 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(1,
                     if constexpr (l <= D - 2) dq[l][H0][r] = dv;
                     else dl[r] = dv;
                 } else {
-                    v[r] = upd(lc, ctr, pw, lp, ocm[r], ocf[r]);
+                    v[r] = upd(lc, ctr, pw, lp, ocm[r]);
                 }
                 if constexpr (l <= D - 2) {
                     u[l][S0][r] = v[r];
@@ -744,7 +743,7 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(1,
                                 cv = (ctr + dv) * rcm[s];
                                 if constexpr (l <= D - 3) rdq[s][l][H0] = dv;
                             } else {
-                                cv = upd(lc, ctr, pw, lp, rcm[s], rcf[s]);
+                                cv = upd(lc, ctr, pw, lp, rcm[s]);
                             }
                             if constexpr (l <= D - 3) ru[s][l][S0] = cv;
                             Up(Ic<l + 1>{}, Ic<H0>{})[Gm::at(l + 1, ry[s], rx[s])] = cv;
@@ -947,9 +946,9 @@ void launch_tbn(int depth, int rows, int waves, bool fm, bool first, const T* A,
     for (int l = 0; l < depth; ++l) {
         p.coef[l] = T(c[l].coef), p.ct[l] = T(c[l].ct), p.ict[l] = T(1 / std::fabs(c[l].ct));
         p.err[l] = err[l];
-        W3D_REQUIRE(l == 0 || c[l].coef == c[1].coef, "tbn: the later layers share one coefficient");
+        W3D_REQUIRE(!fm || l == 0 || c[l].coef == c[1].coef, "tbn --math fma: the later layers share one coefficient");
     }
-    W3D_REQUIRE(first || c[0].coef == c[1].coef, "tbn: one coefficient after the first sweep");
+    W3D_REQUIRE(!fm || first || c[0].coef == c[1].coef, "tbn --math fma: one coefficient after the first sweep");
     auto fcoefs = [](const StepCoefs& q, T out[3]) {
         out[0] = T(q.coef / q.hx2), out[1] = T(q.coef / q.hy2), out[2] = T(q.coef / q.hz2);
     };
