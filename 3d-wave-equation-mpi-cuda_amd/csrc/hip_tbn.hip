@@ -50,11 +50,6 @@
 
 #include "device_common.hpp"
 
-// A/B: B slots (3: two planes of lookahead, runtime slot index; 2: one plane, B issued first:
-// +0.6 % fma, +1.2 % exact, profiles/deep_sweeps_r5.txt)
-#ifndef W3D_TBN_NB
-#define W3D_TBN_NB 2
-#endif
 // Timing ablation (wrong error tables): no error reduction in the planes (what the fused errors
 // cost: profiles/deep_sweeps_r5.txt)
 #ifndef W3D_TBN_ABL_ERR
@@ -136,7 +131,7 @@ struct TbnGeom {
     static constexpr int a_off(int q) { return q * scells; }
     static constexpr int b_off(int q) { return 4 * scells + q * bcells; }
     static constexpr int u_off(int s, int h) {
-        return s == 1 ? b_off(W3D_TBN_NB) + h * cells(1) : u_off(s - 1, 1) + cells(s - 1) + h * cells(s);
+        return s == 1 ? b_off(2) + h * cells(1) : u_off(s - 1, 1) + cells(s - 1) + h * cells(s);
     }
     static constexpr int total = u_off(D - 1, 1) + cells(D - 1);
     // computed positions of ring r: rings 1..D-2 whole, D-1 without corners
@@ -261,7 +256,7 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(1,
     // writes; fp32 one array (measured faster there, profiles/deep_sweeps_r4.txt batches 21/30)
     constexpr bool ONE = sizeof(T) == 4;
     __shared__ T lds[ONE ? Gm::total : 1];
-    constexpr int ZA = ONE ? 1 : Gm::scells, ZB = ONE ? 1 : W3D_TBN_NB * Gm::bcells, Z1 = ONE ? 1 : Gm::cells(1);
+    constexpr int ZA = ONE ? 1 : Gm::scells, ZB = ONE ? 1 : 2 * Gm::bcells, Z1 = ONE ? 1 : Gm::cells(1);
     constexpr int Z2 = ONE || D <= 2 ? 1 : Gm::cells(2), Z3 = ONE || D <= 3 ? 1 : Gm::cells(3);
     __shared__ T tA0[ZA], tA1[ZA], tA2[ZA], tA3[ZA], tB[ZB];
     __shared__ T t10[Z1], t11[Z1], t20[Z2], t21[Z2], t30[Z3], t31[Z3];
@@ -458,10 +453,7 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(1,
     fillA(Ic<0>{}, i0, true);
     fillA(Ic<1>{}, i0 + 1, true);
     fillA(Ic<2>{}, i0 + 2, true);
-    if constexpr (!FIRST) {
-        fillB(0, i0, true);
-        if constexpr (W3D_TBN_NB == 3) fillB(1, i0 + 1, true);
-    }
+    if constexpr (!FIRST) fillB(0, i0, true);
     vm_wait<0>();
     __syncthreads();
     T aw[2][R], raw[2][RP];  // A of the own rows / ring slots in a plane-parity slot (iteration i: A(i) in i - i0 & 1)
@@ -587,27 +579,22 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(1,
         constexpr bool FAST = !ALIAS;
         constexpr int S0 = P & 3, S1 = (P + 1) & 3, S2 = (P + 2) & 3, S3 = (P + 3) & 3;
         constexpr int H0 = P & 1, H1 = (P + 1) & 1;
-        // A(i) .. A(i+3) in A slots S0 .. S3; B(i) in B slot bq, B(i+2) into bq + 2 (mod 3)
-        const int bq = W3D_TBN_NB == 3 ? (i - i0) % 3 : H0;
+        // A(i) .. A(i+3) in A slots S0 .. S3; B(i) in B slot H0, B(i+1) into H1 (two B slots, B
+        // issued first: +0.6 % fma, +1.2 % exact against three slots with two planes of
+        // lookahead, profiles/deep_sweeps_r5.txt)
 
-        // ---- what iteration i-2 issued has landed (A(i+1), B(i); the checked body waits for
-        // everything) -> barrier -> DMA A(i+3), B(i+2) into the slots of A(i-1), B(i-1), whose
-        // last readers passed the barrier
-        // (NB = 2: iteration i-1 issued B(i) first — wait for it and what came before, leaving
-        // its A pieces and stores in flight)
+        // ---- what iteration i-2 issued has landed (A(i+1); the checked body waits for
+        // everything), and B(i), which iteration i-1 issued first (wait for it and what came
+        // before, leaving its A pieces and stores in flight) -> barrier -> DMA B(i+1), A(i+3)
+        // into the slots of B(i-1), A(i-1), whose last readers passed the barrier
         constexpr int NA = (ES == 8 ? 1 : 2) * Gm::RPW;
-        if constexpr (FAST && W3D_TBN_NB == 2 && !FIRST) vm_wait<NA + NST>();
+        if constexpr (FAST && !FIRST) vm_wait<NA + NST>();
         else if constexpr (FAST) vm_wait<NDMA + 2 * NST>();
         else vm_wait<0>();
         __syncthreads();
         // (issued right here: later in the plane measured 7-16 % slower)
-        if constexpr (W3D_TBN_NB == 2) {
-            if constexpr (!FIRST) fillB(H1, i + 1, FAST || i + 1 <= ie + D - 1);
-            fillA(Ic<S3>{}, i + 3, FAST || i + 3 <= ie + D);
-        } else {
-            fillA(Ic<S3>{}, i + 3, FAST || i + 3 <= ie + D);
-            if constexpr (!FIRST) fillB(bq == 0 ? 2 : bq - 1, i + 2, FAST || i + 2 <= ie + D - 1);
-        }
+        if constexpr (!FIRST) fillB(H1, i + 1, FAST || i + 1 <= ie + D - 1);
+        fillA(Ic<S3>{}, i + 3, FAST || i + 3 <= ie + D);
 
         T ev[R];  // U_{D-1}(i - D + 1): stored and its errors taken below
 #pragma unroll
@@ -639,7 +626,7 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(1,
                 g.gz[r][0] = St(lc, o - 1), g.gz[r][1] = St(lc, o + 1);
                 if constexpr (l == 0) {
                     g.gc[r] = ldsr(Ap(Ic<S0>{}), oA), g.gxp[r] = ldsr(Ap(Ic<S1>{}), oA);
-                    if constexpr (!FIRST) g.gpw[r] = ldsr(Bp(bq), Gm::bat(y, xx));
+                    if constexpr (!FIRST) g.gpw[r] = ldsr(Bp(H0), Gm::bat(y, xx));
                 }
             }
             if constexpr (l <= D - 2)
@@ -651,7 +638,7 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(1,
                         g.grn[s][2] = St(lc, ro - 1), g.grn[s][3] = St(lc, ro + 1);
                         if constexpr (l == 0) {
                             g.grc[s] = ldsr(Ap(Ic<S0>{}), ro0[s]), g.grxp[s] = ldsr(Ap(Ic<S1>{}), ro0[s]);
-                            if constexpr (!FIRST) g.grpw[s] = ldsr(Bp(bq), rb0[s]);
+                            if constexpr (!FIRST) g.grpw[s] = ldsr(Bp(H0), rb0[s]);
                         }
                     }
                 });
