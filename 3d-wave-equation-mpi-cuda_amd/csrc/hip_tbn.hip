@@ -242,7 +242,10 @@ __device__ __forceinline__ void vm_wait() {
 // one layer to the next (same plane, next iteration) and never in LDS. The sweep stores d and U of
 // its last layer (O[0] = the next sweep's B, O[1] its A), with the last layer's self-wrap ranges.
 template <class T, int D, bool FIRST, int R, int NW, bool FM, bool DELTA = false>
-__global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(1, 8))) k_tbn(const TbnParams<T> p) {
+// fp32: at least 4 waves per SIMD, i.e. two workgroups per CU (LDS 75 KB each): the increment
+// form's 132 VGPRs had dropped it to one (634k vs 872-878k Mpts/s at N=512, deep_sweeps_r5.txt)
+__global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(sizeof(T) == 4 ? 4 : 1, 8)))
+k_tbn(const TbnParams<T> p) {
     constexpr int TJ = NW * R;
     constexpr int ES = sizeof(T);
     using Gm = TbnGeom<D, TJ, ES, NW>;

@@ -48,7 +48,10 @@ Layout plan_layout(const Config& c, int world) {
     // (profiles/deep_sweeps_r4.txt). The increment form runs on tb3 (k_tbn's fp32 one is slower),
     // since round 4 the fp64 exact one too: 378-379k vs tb2r2w4 298k Mpts/s at N=512 after tb3's
     // register j-neighbours and the max-ilp build (deep_sweeps_r4.txt batch 33).
-    const bool auto_tb4 = auto_tb && !c.delta;
+    // Round 5: the fp32 increment form with --math fma runs on tb4 too, two workgroups per CU:
+    // 872-878k vs tb3 787-790k Mpts/s at N=512 (exact stays on tb3: 766k vs 675k;
+    // profiles/deep_sweeps_r5.txt)
+    const bool auto_tb4 = auto_tb && (!c.delta || (c.dtype == DType::F32 && c.fma));
     const bool auto_tb3 = auto_tb && !auto_tb4;
     const bool tbn3 = c.kernel.rfind("tbn3", 0) == 0;  // k_tbn at depth 3 (A/B of k_tb3)
     const bool tb4 = auto_tb4 || c.kernel.rfind("tb4", 0) == 0;
