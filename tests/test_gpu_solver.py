@@ -423,6 +423,21 @@ def test_fp32_auto_is_tb4_bitwise(C):
     assert multi.max_abs == ref.max_abs and multi.max_rel == ref.max_rel
 
 
+@pytest.mark.parametrize("math_,want", [("fma", "tb4"), ("exact", "tb3")])
+def test_fp32_delta_auto_kernel(C, math_, want):
+    """The fp32 increment form's "auto" sweep: tb4 with --math fma (two workgroups per CU since
+    round 5, 872-878k vs tb3 787-790k at N=512, profiles/deep_sweeps_r5.txt step 13), tb3 in
+    exact arithmetic; both at the OpenMP oracle's max abs errors."""
+    import wave3d
+
+    p = wave3d.WaveProblem(29, Lx=1.3, Ly="pi", Lz=2.0, timesteps=13, ic="shifted", dtype="fp32",
+                           scheme="delta", math=math_)
+    ref = _solve(p, backend="cpu", threads=4)
+    got = _solve(p)
+    assert got.kernel == want and got.extra["scheme"] == "delta"
+    assert got.max_abs == ref.max_abs
+
+
 @pytest.mark.parametrize("kernel,scheme", [("tb2", "leapfrog"), ("tb3", "leapfrog"), ("march2", "leapfrog"),
                                            ("tb2", "delta")])
 @pytest.mark.parametrize("dims", ["2,2,2", "1,2,2"])
