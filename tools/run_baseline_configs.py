@@ -63,7 +63,8 @@ def main():
             r = wave3d.WaveSolver(p, be, Np=Np, dims=dims).run(repeat=a.repeat, warmup=1)
             mpts, linf, d = r.mpts_per_s_best, r.linf_abs, r.dims
         elif sim:
-            r = wave3d.WaveSolver(p, be, ranks=Np, dims=dims).run(repeat=a.repeat, warmup=1)
+            # --overlap auto as bench.py: solves 2-7 time the arms (untimed warm-ups here)
+            r = wave3d.WaveSolver(p, be, ranks=Np, dims=dims, overlap="auto").run(repeat=a.repeat, warmup=7)
             mpts, linf, d = r.mpts_per_s_best, r.linf_abs, r.dims
             be = "hip-sim"
         else:
