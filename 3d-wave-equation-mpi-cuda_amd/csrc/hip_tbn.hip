@@ -56,7 +56,18 @@
 #define W3D_TBN_ABL_ERR 0
 #endif
 
+// W3D_TBN_PART 2 (hip_tbn_exact.hip): only the --math exact instantiations, in an object of
+// their own under LLVM's max-memory-clause scheduler; the fma ones keep max-ilp (Makefile,
+// profiles/deep_sweeps_r5.txt step 16)
+#ifndef W3D_TBN_PART
+#define W3D_TBN_PART 1
+#endif
+
 namespace wave3d {
+// the --math exact kernel of a depth / first-sweep / scheme (hip_tbn_exact.hip), a kernel stub
+template <class T>
+const void* tbn_exact_kernel(int depth, bool first, bool delta);
+
 namespace {
 
 template <class F, int... I>
@@ -863,16 +874,24 @@ k_tbn(const TbnParams<T> p) {
     });
 }
 
+// the kernel of one math mode; the increment form: fp32 at depth 4 (config 5's scheme; fp64 uses
+// the leapfrog)
+template <class T, int D, bool F, bool FM>
+static const void* tbn_kernel_m(bool delta) {
+    if (delta) {
+        if constexpr (std::is_same_v<T, float> && D == 4)
+            return reinterpret_cast<const void*>(k_tbn<T, D, F, 2, 8, FM, true>);
+        return nullptr;
+    }
+    return reinterpret_cast<const void*>(k_tbn<T, D, F, 2, 8, FM>);
+}
+
+#if W3D_TBN_PART == 1
 template <class T, int D, bool F>
 static void (*tbn_kernel(int rows, int waves, bool fm, bool delta))(const TbnParams<T>) {
     if (rows != 2 || waves != 8) return nullptr;
-    // the increment form: fp32 at depth 4 (config 5's scheme; fp64 uses the leapfrog)
-    if (delta) {
-        if constexpr (std::is_same_v<T, float> && D == 4)
-            return fm ? k_tbn<T, D, F, 2, 8, true, true> : k_tbn<T, D, F, 2, 8, false, true>;
-        return nullptr;
-    }
-    return fm ? k_tbn<T, D, F, 2, 8, true> : k_tbn<T, D, F, 2, 8, false>;
+    const void* k = fm ? tbn_kernel_m<T, D, F, true>(delta) : tbn_exact_kernel<T>(D, F, delta);
+    return reinterpret_cast<void (*)(const TbnParams<T>)>(const_cast<void*>(k));
 }
 
 template <class T, bool F>
@@ -882,9 +901,21 @@ static void (*tbn_kernel_d(int depth, int rows, int waves, bool fm, bool delta =
         if (depth == 3) return tbn_kernel<T, 3, F>(rows, waves, fm, delta);
     return nullptr;
 }
+#endif
 
 }  // namespace
 
+#if W3D_TBN_PART == 2
+template <class T>
+const void* tbn_exact_kernel(int depth, bool first, bool delta) {
+    if (depth == 4) return first ? tbn_kernel_m<T, 4, true, false>(delta) : tbn_kernel_m<T, 4, false, false>(delta);
+    if constexpr (std::is_same_v<T, double>)  // depth 3: fp64 (the cross-check of k_tb3, A/B)
+        if (depth == 3) return first ? tbn_kernel_m<T, 3, true, false>(delta) : tbn_kernel_m<T, 3, false, false>(delta);
+    return nullptr;
+}
+template const void* tbn_exact_kernel<double>(int, bool, bool);
+template const void* tbn_exact_kernel<float>(int, bool, bool);
+#else
 bool tbn_supported(int depth, int rows, int waves, bool fm, bool fp32) {
     return fp32 ? tbn_kernel_d<float, false>(depth, rows, waves, fm) != nullptr
                 : tbn_kernel_d<double, false>(depth, rows, waves, fm) != nullptr;
@@ -993,5 +1024,6 @@ void launch_tbn(int depth, int rows, int waves, bool fm, bool first, const T* A,
                                 u64* const*, int, hipStream_t, bool);
 W3D_TBN_INST(double)
 W3D_TBN_INST(float)
+#endif
 
 }  // namespace wave3d
