@@ -283,7 +283,7 @@ k_tbn(const TbnParams<T> p) {
         else if constexpr (q == 2) return tA2;
         else return tA3;
     };
-    // B slot q (runtime: B(x) in slot (x - i0) mod 3)
+    // B slot q (B(x) in slot (x - i0) & 1)
     auto Bp = [&](int q) -> T* {
         if constexpr (ONE) return lds + Gm::b_off(0) + q * Gm::bcells;
         else return tB + q * Gm::bcells;
@@ -380,7 +380,7 @@ k_tbn(const TbnParams<T> p) {
         if (p.w_lo[1][g] <= ie && p.w_hi[1][g] >= ib) rare |= 2;
     }
     rare = __builtin_amdgcn_readfirstlane(rare);
-    // steady-state window [flo, fhi]: every layer on an own-range plane, A(i+3) / B(i+2) still
+    // steady-state window [flo, fhi]: every layer on an own-range plane, A(i+3) / B(i+1) still
     // inside the work item, off the periodic seam and the self-wrap planes (those sit at the
     // ends of the x range, so each one trims the window from its nearer end)
     int flo = ib + D - 1, fhi = ie + D - 3;
@@ -451,17 +451,17 @@ k_tbn(const TbnParams<T> p) {
         dma_fill3<ES, Gm::W(1) * ES, Gm::browb>(prs(p.B, plane, live ? pbytes : 0u), src0 + ES, sjb,
                                                 __builtin_amdgcn_readfirstlane(lds_addr(Bp(q))), bds0);
     };
-    // Two planes of lookahead for A and B: A(x) in A slot (x - i0) & 3 — A(i), A(i+1) read at
-    // iteration i, A(i+2) in flight, A(i+3) issued into the slot of A(i-1), whose own-node and
+    // Two planes of lookahead for A, one for B: A(x) in A slot (x - i0) & 3 — A(i), A(i+1) read
+    // at iteration i, A(i+2) in flight, A(i+3) issued into the slot of A(i-1), whose own-node and
     // ring values ride in registers from the last iteration (aw / raw: its x- neighbour for layer
-    // 0, U_{-1} for layer 1); B(x) in B slot (x - i0) mod 3 — B(i) read, B(i+1) in flight, B(i+2)
-    // issued into the slot of B(i-1). Each iteration issues its A pieces, then its B pieces, then
-    // its stores; a steady iteration waits for what iteration i-2 issued, i.e. for all but the
-    // operations of iteration i-1 and the stores of i-2: NDMA + 2 NST.
+    // 0, U_{-1} for layer 1); B(x) in B slot (x - i0) & 1 — B(i) read, B(i+1) issued into the slot
+    // of B(i-1). Each iteration issues its B piece first, then its A pieces, then its stores; a
+    // steady iteration waits for B(i) and what came before it, i.e. for all but the A pieces and
+    // stores of iteration i-1: NA + NST (the first sweep, with no B: NDMA + 2 NST).
     constexpr int NST = 2 * R;                                  // stores of the last two layers
     // pieces per iteration: A, and B unless this is the first sweep (which reads no B)
     constexpr int NDMA = (ES == 8 ? 1 : 2) * Gm::RPW * (FIRST ? 1 : 2);
-    // prologue: A(i0-1) .. A(i0+2) into slots 3, 0, 1, 2; B(i0), B(i0+1) into slots 0, 1; then
+    // prologue: A(i0-1) .. A(i0+2) into slots 3, 0, 1, 2; B(i0) into slot 0; then
     // A(i0-1)'s register copies
     fillA(Ic<3>{}, i0 - 1, true);
     fillA(Ic<0>{}, i0, true);
