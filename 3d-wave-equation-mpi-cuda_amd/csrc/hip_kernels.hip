@@ -382,32 +382,44 @@ __global__ void __launch_bounds__(kThreads) k_flat(const StepParams<T> p) {
 }
 
 // ---------------------------------------------------------------------------------------
-// Layer 0 (initial condition): one workgroup per 4 x 64 (j,k) tile and `chunk` planes.
+// Layer 0 (initial condition): one workgroup per 4 rows (a wave each, its lanes along the whole
+// k range) and `chunk` planes, so consecutive workgroups write consecutive rows of a plane in
+// long runs (4 x 64 tiles wrote 512-B pieces one plane apart): 258-272 vs 278-301 us at N=512,
+// non-temporal stores no better (profiles/deep_sweeps_r5.txt step 17).
 template <class T>
 __global__ void __launch_bounds__(kThreads) k_init(T* u, i64 si, int sj, Box bx, int chunk,
                                                    Wrap wrap, const T* tx, const T* ty,
                                                    const T* tz, T ct, u64* err) {
-    const int k = bx.k0 + blockIdx.x * 64 + (threadIdx.x & 63);
-    const int j = bx.j0 + blockIdx.y * kWaves + (threadIdx.x >> 6);
-    const int ib = bx.i0 + blockIdx.z * chunk;
+    const int lane = threadIdx.x & 63;
+    const int j = bx.j0 + blockIdx.x * kWaves + (threadIdx.x >> 6);
+    const int ib = bx.i0 + blockIdx.y * chunk;
     const int ie = min(bx.i1, ib + chunk - 1);
-    T ma = T(kErrInit);
-    RelArg<T> mr;
+    // layer 0 is the analytic solution itself: every error is exactly 0 (the reference's
+    // |f - f| and |f - f| / |f|); the relative one only where f != 0 (0/0 is NaN, which its `>`
+    // ignores) — the same maxima as accumulate_error_dev without its per-node work
+    T ma = T(kErrInit), mr = T(kErrInit);
     T chk = T(0);  // sum of the values (commit_errors: nonfinite flag)
-    if (k <= bx.k1 && j <= bx.j1) {
-        const int rowoff = j * sj + k;
-        const T tyj = ty[j], tzk = tz[k];
+    if (j <= bx.j1) {
+        const T tyj = ty[j];
+        bool nz = false, any = false;
         for (int i = ib; i <= ie; ++i) {
-            const T f = analytic(tx[i], tyj, tzk, ct);
-            u[i64(i) * si + rowoff] = f;
+            const T txi = tx[i];
+            const i64 row = i64(j) * sj;
+            for (int k = bx.k0 + lane; k <= bx.k1; k += 64) {
+                const T f = analytic(txi, tyj, tz[k], ct);
+                u[i64(i) * si + row + k] = f;
 #pragma unroll
-            for (int q = 0; q < kMaxWrap; ++q)
-                if (i == wrap.src[q]) u[i64(wrap.dst[q]) * si + rowoff] = f;
-            chk += f;
-            accumulate_error_dev(f, analytic(tx[i], tyj, tzk, ct), ma, mr);
+                for (int q = 0; q < kMaxWrap; ++q)  // wrap copies of this plane (uniform tests)
+                    if (i == wrap.src[q]) u[i64(wrap.dst[q]) * si + row + k] = f;
+                chk += f;
+                nz |= f != T(0);
+                any = true;
+            }
         }
+        if (any) ma = T(0);
+        if (nz) mr = T(0);
     }
-    commit_errors(ma, mr.value(), chk, err);
+    commit_errors(ma, mr, chk, err);
 }
 
 template <class T>
@@ -701,9 +713,9 @@ void launch_init(T* u, const GridView& gv, const Box& bx, const Wrap& wrap, cons
     W3D_REQUIRE(bx.i0 >= 1 && bx.i1 <= gv.X && bx.j1 <= gv.Y && bx.k1 <= gv.Z,
                 "init box outside the owned region");
     const int planes = bx.i1 - bx.i0 + 1;
-    const int tiles = cdiv(bx.k1 - bx.k0 + 1, 64) * cdiv(bx.j1 - bx.j0 + 1, kWaves);
-    const int chunk = std::min(planes, std::max(1, cdiv(planes * tiles, 4096)));
-    dim3 grid(cdiv(bx.k1 - bx.k0 + 1, 64), cdiv(bx.j1 - bx.j0 + 1, kWaves), cdiv(planes, chunk));
+    const int rowblocks = cdiv(bx.j1 - bx.j0 + 1, kWaves);
+    const int chunk = std::min(planes, std::max(1, cdiv(planes * rowblocks, 4096)));
+    dim3 grid(rowblocks, cdiv(planes, chunk));
     hipLaunchKernelGGL(k_init<T>, grid, dim3(kThreads), 0, s, u, gv.si, gv.sj, bx, chunk, wrap, tx,
                        ty, tz, T(ct0), err);
     HIP_OK(hipGetLastError());
