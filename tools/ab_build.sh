@@ -8,6 +8,8 @@ cd "$(dirname "$0")/../3d-wave-equation-mpi-cuda_amd"
 ROCM=/opt/rocm
 FLAGS="-O3 -std=c++17 -fPIC -ffp-contract=off -Wall -Wno-unknown-pragmas --offload-arch=gfx950 -fopenmp -munsafe-fp-atomics -I$ROCM/include -Wno-pass-failed"
 srcs=${1//,/ }; shift
+# hip_tbn_exact.hip includes hip_tbn.hip (the --math exact kernels): a hip_tbn variant rebuilds both
+case " $srcs " in *" hip_tbn "*) case " $srcs " in *" hip_tbn_exact "*) ;; *) srcs="$srcs hip_tbn_exact";; esac;; esac
 objs=$(ls build/hip/*.o)
 for src in $srcs; do objs=$(echo "$objs" | grep -v "/$src.o\$"); done
 for v in "$@"; do
