@@ -79,11 +79,9 @@ struct TbParams {
 // constant, so no value ever moves between registers: a prefetch load lands in the slot it
 // is consumed from two planes later, and the compiler needs no s_waitcnt vmcnt(0) to copy
 // an in-flight register (the rotate-by-copy form serialised every plane on load latency).
-// ABL (measurement ablation, env WAVE3D_TB_ABLATION, not a solver mode): 1 = no error
-// reduction at all, 2 = absolute error only (no relative-error division).
 // C and D are written with the non-temporal policy (+3-5 % at N=512,
-// profiles/sweep_store_policy_r1.txt). OPT (env WAVE3D_TB_OPT, A/B ablation, bitwise-
-// neutral): 1 = default-policy stores instead. (Prefetch distances: own A and both A rings 2
+// profiles/sweep_store_policy_r1.txt; the error-reduction ablations of round 1 are in
+// profiles/sweep_n512_tb_variants_r1.txt). (Prefetch distances: own A and both A rings 2
 // planes, B 1 plane; B at distance 2 measured no faster, the outer ring at distance 2 +2.6 %.)
 // DELTA: increment form (csrc/hip_kernels.hpp launch_tb2): B = d^{m-1}; d^m = B + coefC*lap A,
 // C = A + d^m (registers: errors, D's stencil); d^{m+1} = d^m + coefD*lap C, D = C + d^{m+1};
@@ -94,7 +92,7 @@ struct TbParams {
 // XCD, so they are fetched again from beyond L2 — the bulk of tb2's read surplus,
 // profiles/dram_bytes_r2.txt).
 // FM: --math fma (stencil_math coef_lap_fma), as k_tb3.
-template <class T, bool FIRST, int R, int NW, int WPE = 1, int ABL = 0, int OPT = 0, bool DELTA = false,
+template <class T, bool FIRST, int R, int NW, int WPE = 1, bool DELTA = false,
           int NWK = 1, bool FM = false>
 __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WPE, 8))) k_tb2(const TbParams<T> p) {
     static_assert(NW % NWK == 0, "waves along k must divide the workgroup");
@@ -104,7 +102,7 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WP
     constexpr int AH = TJ + 4, AW = TK + 4;   // A tile: rows jt-2..jt+TJ+1, cols kb-2..kb+TK+1
     constexpr int CH = TJ + 2, CW = TK + 2;   // C tile: rows jt-1..jt+TJ,   cols kb-1..kb+TK
     constexpr unsigned ES = sizeof(T);
-    constexpr int kStAux = (OPT & 1) ? 0 : 2;  // store cache policy: 2 = non-temporal
+    constexpr int kStAux = 2;  // store cache policy: non-temporal
     static_assert(2 * TK + 2 * CH <= NW * 64 && 2 * (TK + 2) + 2 * CH <= NW * 64, "ring needs more lanes");
     __shared__ T ldsA[2][AH][AW];
     __shared__ T ldsC[2][CH][CW];
@@ -295,7 +293,6 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WP
     // errors and finiteness sum of one own plane i of a layer (values v[r]); the uniform plane
     // test outside the per-lane row masks keeps it a scalar branch
     auto errors_exact = [&](const T(&v)[R], const int i, const T ct, T& ma, auto& mr, T& chk) {
-        if constexpr (ABL == 1) return;
         if (eplane(i)) {
             const T* const trow = txw + i * p.tpj;
 #pragma unroll
@@ -303,12 +300,7 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WP
                 if (!ovalid[r]) continue;
                 chk += v[r];
                 const T f = (ldconst(trow, r) * otz) * ct;  // = ((sx*sy)*sz)*ct, stencil_math analytic
-                if constexpr (ABL == 2) {
-                    const T e = absval(v[r] - f);
-                    if (e > ma) ma = e;
-                } else {
-                    accumulate_error_dev(v[r], f, ma, mr);
-                }
+                accumulate_error_dev(v[r], f, ma, mr);
             }
         } else {
 #pragma unroll
@@ -516,9 +508,9 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WP
 template <class T, bool F>
 static void (*tb_fma_kernel(int rows, int waves, int nwk, bool delta))(const TbParams<T>) {
     switch (rows * 100 + waves * 10 + nwk + (delta ? 10000 : 0)) {
-        case 281: return k_tb2<T, F, 2, 8, 1, 0, 0, false, 1, true>;
-        case 241: return k_tb2<T, F, 2, 4, 1, 0, 0, false, 1, true>;
-        case 10281: return k_tb2<T, F, 2, 8, 1, 0, 0, true, 1, true>;
+        case 281: return k_tb2<T, F, 2, 8, 1, false, 1, true>;
+        case 241: return k_tb2<T, F, 2, 4, 1, false, 1, true>;
+        case 10281: return k_tb2<T, F, 2, 8, 1, true, 1, true>;
         default: return nullptr;
     }
 }
@@ -530,10 +522,10 @@ bool tb2_fma_supported(int rows, int waves, int nwk, bool delta) {
 template <class T, bool F>
 static void (*tb_delta_kernel(int rows, int waves, int nwk))(const TbParams<T>) {
     switch (rows * 100 + waves * 10 + nwk) {
-        case 241: return k_tb2<T, F, 2, 4, 1, 0, 0, true>;
-        case 281: return k_tb2<T, F, 2, 8, 1, 0, 0, true>;
-        case 441: return k_tb2<T, F, 4, 4, 1, 0, 0, true>;
-        case 282: return k_tb2<T, F, 2, 8, 1, 0, 0, true, 2>;
+        case 241: return k_tb2<T, F, 2, 4, 1, true>;
+        case 281: return k_tb2<T, F, 2, 8, 1, true>;
+        case 441: return k_tb2<T, F, 4, 4, 1, true>;
+        case 282: return k_tb2<T, F, 2, 8, 1, true, 2>;
         default: return nullptr;
     }
 }
@@ -547,24 +539,11 @@ template <class T, bool F>
 static void (*tb_kernel(int rows, int waves, int occ, int nwk))(const TbParams<T>) {
     switch (rows * 1000 + waves * 10 + occ + (nwk - 1) * 100000) {
         // 128-column tiles (two waves side by side along k)
-        case 102080: return k_tb2<T, F, 2, 8, 1, 0, 0, false, 2>;
-        case 102084: return k_tb2<T, F, 2, 8, 4, 0, 0, false, 2>;
-        case 104080: return k_tb2<T, F, 4, 8, 1, 0, 0, false, 2>;
-        case 102160: return k_tb2<T, F, 2, 16, 1, 0, 0, false, 2>;
-        case 2040: {
-            static const int abl = [] {
-                const char* e = std::getenv("WAVE3D_TB_ABLATION");
-                return e ? std::atoi(e) : 0;
-            }();
-            static const int opt = [] {
-                const char* e = std::getenv("WAVE3D_TB_OPT");
-                return e ? std::atoi(e) : 0;
-            }();
-            if (abl == 1) return k_tb2<T, F, 2, 4, 1, 1>;
-            if (abl == 2) return k_tb2<T, F, 2, 4, 1, 2>;
-            if (opt == 1) return k_tb2<T, F, 2, 4, 1, 0, 1>;
-            return k_tb2<T, F, 2, 4>;
-        }
+        case 102080: return k_tb2<T, F, 2, 8, 1, false, 2>;
+        case 102084: return k_tb2<T, F, 2, 8, 4, false, 2>;
+        case 104080: return k_tb2<T, F, 4, 8, 1, false, 2>;
+        case 102160: return k_tb2<T, F, 2, 16, 1, false, 2>;
+        case 2040: return k_tb2<T, F, 2, 4>;
         case 2044: return k_tb2<T, F, 2, 4, 4>;
         case 2045: return k_tb2<T, F, 2, 4, 5>;
         case 4040: return k_tb2<T, F, 4, 4>;

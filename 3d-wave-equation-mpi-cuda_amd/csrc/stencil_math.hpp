@@ -160,16 +160,13 @@ W3D_HD T leapfrog_fma(T c, T u2, T l) {
 // 8 operations) biases the rounding of the O(|u|) sum and grows quadratically under the leapfrog:
 // 6.03381562e-07, which breaks the printed golden. fp32 keeps the composition above: its accuracy
 // rests on the exact (Sterbenz) differences. kc = fm_kc(cx, cy, cz), loop-invariant.
-#ifndef W3D_FM_FUSED  // A/B: 0 = fp64 --math fma leapfrog as coef_lap_fma + leapfrog_fma
-#define W3D_FM_FUSED 1
-#endif
 template <class T>
 W3D_HD T fm_kc(T cx, T cy, T cz) {
     return T(-2) * ((cx + cy) + cz);
 }
 template <class T>
 W3D_HD T leap_fm(T c, T u2, T xm, T xp, T ym, T yp, T zm, T zp, T cx, T cy, T cz, T kc) {
-    if constexpr (W3D_FM_FUSED && std::is_same_v<T, double>) {
+    if constexpr (std::is_same_v<T, double>) {
         T t = cz * (zm + zp);
         t = fma_t(cy, ym + yp, t);
         t = fma_t(cx, xm + xp, t);
@@ -185,7 +182,7 @@ W3D_HD T leap_fm(T c, T u2, T xm, T xp, T ym, T yp, T zm, T zp, T cx, T cy, T cz
 // never stored), so the result is 0 without a product per node
 template <class T>
 W3D_HD T leap_fm_masked(T c, T u2, T xm, T xp, T ym, T yp, T zm, T zp, T cx, T cy, T cz, T kc, T m) {
-    if constexpr (W3D_FM_FUSED && std::is_same_v<T, double>) {
+    if constexpr (std::is_same_v<T, double>) {
         T t = cz * (zm + zp);
         t = fma_t(cy, ym + yp, t);
         t = fma_t(cx, xm + xp, t);
