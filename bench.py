@@ -52,8 +52,9 @@ def main() -> int:
                     help="run a named BASELINE config instead (models/presets.py CONFIGS, e.g. "
                          "gpu2048x8_fp32 = config 5: N, timesteps, dtype, decomposition)")
     ap.add_argument("--dims", default="", help="process grid a,b,c (default: the BASELINE config's)")
-    ap.add_argument("--timesteps", type=int, default=100,
-                    help="layers per solve (0: smallest stable count with margin, C <= 0.5)")
+    ap.add_argument("--timesteps", type=int, default=None,
+                    help="layers per solve (default 100; with --fill-hbm 0; 0: smallest stable count with "
+                         "margin, C <= 0.5)")
     ap.add_argument("--fill-hbm", type=float, default=0.0,
                     help="size N to this fraction of each GPU's HBM (SURVEY §7.3; e.g. 0.9)")
     ap.add_argument("--dtype", default="fp64", choices=["fp64", "fp32"])
@@ -149,6 +150,8 @@ def main() -> int:
         plan = dict(plan, config=a.config, golden=presets.GOLDEN_LINF.get((np_.N, np_.timesteps)))
     N = a.N or plan["N"]
     dims = [int(x) for x in a.dims.split(",")] if a.dims else (None if a.N else plan["dims"])
+    if a.timesteps is None:  # --fill-hbm moves N: keep the run stable unless K is given
+        a.timesteps = 0 if a.fill_hbm > 0 else 100
     if a.fill_hbm > 0:
         if a.backend != "hip":
             print("bench: --fill-hbm needs the hip backend", file=sys.stderr)
